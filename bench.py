@@ -1,0 +1,204 @@
+#!/usr/bin/env python
+"""Benchmark: GPT-2 training step (fwd + bwd + grad all-reduce + AdamW) on N MI355X GPUs.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 launched by
+``torch.distributed.run`` (one rank per GPU, RCCL). W untimed warm-up steps, then EXACTLY K steps
+bracketed by barrier + synchronize, wall time = MAX over ranks; rank 0 prints ONE JSON line.
+
+Workload = BASELINE.json config 2/3: GPT-2 124M (12L/768d/12H, V=50257), B=64 sequences per GPU,
+T=1024, bf16 compute (autocast numerics), fp32 master weights, fused AdamW (lr 1e-4, wd 0.1,
+betas 0.9/0.95), dropout 0.1 as the reference's default config (model.py:47-51), grad_accum 1.
+Data: synthetic uniform token batches already resident in HBM (no network).
+
+Also reported:
+  mfu          tok/s * 854,438,400 FLOP/token / (N * 2.5166e15)   (bf16 dense peak)
+  roofline     for the dominant kernel (the tied lm_head GEMMs are the largest launches): algorithmic
+               FLOP per launch / average launch time measured live with HIP events on the launch stream
+  kernels      the same for every probed launch family
+  cpu_baseline the oracle (CPU restatement of the reference step, oracle/train_ref.py) timed on this
+               host's cores on a bounded sample (rank 0, N = 1 only)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+PEAK_BF16_TFLOPS = 256 * 4 * 1024 * 2.4e9 / 1e12  # 2516.6 dense bf16 (MI355X_MICROARCH.md)
+METRIC = "train tokens/sec (whole node) + MFU, GPT-2 124M B=64 T=1024 at 1/2/4/8 MI355X"
+
+
+def flops_per_token(cfg, T):
+    C, L, V = cfg.n_embd, cfg.n_layer, cfg.vocab_size
+    return 6 * (L * 12 * C * C + V * C) + 12 * L * T * C
+
+
+def cpu_baseline(batch=2, seq_len=1024, steps=2):
+    """The oracle's fp32 CPU step (same model/seq_len; bounded sample: B=2, timed after 1 warm-up step)."""
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from oracle import model_ref, train_ref
+    cfg = model_ref.Cfg(resid_pdrop=0.0, attn_pdrop=0.0, n_positions=seq_len)
+    g = torch.Generator().manual_seed(0)
+    data = [(torch.randint(0, cfg.vocab_size, (batch, seq_len), generator=g),
+             torch.randint(0, cfg.vocab_size, (batch, seq_len), generator=g)) for _ in range(steps + 1)]
+    params = model_ref.init_params(cfg)
+    train_ref.run(cfg, data[:1], 1, params=params)  # warm-up (allocations, thread pool)
+    t0 = time.perf_counter()
+    train_ref.run(cfg, data[1:], steps, params=params)
+    dt = time.perf_counter() - t0
+    return {"value": round(steps * batch * seq_len / dt, 2), "unit": "tokens/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"oracle/train_ref.py fp32 fwd+bwd+AdamW, 124M, B={batch}, T={seq_len}, {steps} timed steps "
+                      f"({dt:.1f} s) after 1 warm-up"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--seq_len", type=int, default=1024)
+    ap.add_argument("--model", default="124M")
+    ap.add_argument("--dropout", type=float, default=0.1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--bucket-mb", type=float, default=64.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        from gpt_2_distributed_amd.parallel import init_distributed
+        init_distributed()
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+
+    from gpt_2_distributed_amd.model import GPT2, GPT2Config, MODEL_SIZES
+    cfg = GPT2Config(**MODEL_SIZES[args.model], n_positions=args.seq_len, resid_pdrop=args.dropout,
+                     attn_pdrop=args.dropout)
+    model = GPT2(cfg).to(dev)
+    model.train()
+    if world > 1:
+        from gpt_2_distributed_amd.parallel import DistributedDataParallel
+        ddp = DistributedDataParallel(model, bucket_mb=args.bucket_mb)
+        opt = ddp.configure_optimizers(learning_rate=1e-4)
+        fwd = ddp
+    else:
+        opt = model.configure_optimizers(learning_rate=1e-4)
+        fwd = model
+    eng = model.engine()
+
+    B, T = args.batch, args.seq_len
+    g = torch.Generator().manual_seed(1234 + rank)
+    batches = []
+    for _ in range(4):
+        t = torch.randint(0, cfg.vocab_size, (B, T + 1), generator=g)
+        batches.append((t[:, :-1].contiguous().to(dev), t[:, 1:].contiguous().to(dev)))
+
+    def step(i):
+        x, y = batches[i % len(batches)]
+        _, loss = fwd(x, labels=y)
+        loss.backward()
+        opt.step()
+        opt.zero_grad()
+        return loss
+
+    for i in range(args.warmup):
+        loss = step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    probes = ["lm_head_fwd", "lm_head_dgrad", "lm_head_wgrad", "fc1_fwd", "attn_fwd"]
+    eng.probes = {p: [] for p in probes}
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss = step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    eng.probes, armed = {}, eng.probes
+    dt_t = torch.tensor([dt], device=dev)
+    if world > 1:
+        dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
+    dt = float(dt_t.item())
+    final_loss = float(loss.item())
+
+    M = B * T
+    C, V, H = cfg.n_embd, cfg.vocab_size, cfg.n_head
+    kflops = {
+        "lm_head_fwd": 2.0 * M * V * C, "lm_head_dgrad": 2.0 * M * V * C, "lm_head_wgrad": 2.0 * M * V * C,
+        "fc1_fwd": 2.0 * M * 4 * C * C, "attn_fwd": 4.0 * B * H * (T * (T + 1) / 2) * (C // H),
+    }
+    kernels = {}
+    for name, evs in armed.items():
+        if not evs:
+            continue
+        ms = sum(s.elapsed_time(e) for s, e in evs) / len(evs)
+        tf = kflops[name] / (ms * 1e-3) / 1e12
+        kernels[name] = {"avg_ms": round(ms, 4), "launches": len(evs), "tflops": round(tf, 1),
+                         "frac_of_peak": round(tf / PEAK_BF16_TFLOPS, 4)}
+    dom = max(kernels, key=lambda k: kernels[k]["avg_ms"] * kernels[k]["launches"] / max(1, args.steps)) \
+        if kernels else None
+    traffic = None
+    tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "traffic.json")
+    if dom and os.path.exists(tpath):
+        try:
+            traffic = json.load(open(tpath)).get(dom, {}).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    roofline = None
+    if dom:
+        k = kernels[dom]
+        roofline = {"kernel": dom, "bound": "mfma", "achieved": k["tflops"], "peak": round(PEAK_BF16_TFLOPS, 1),
+                    "unit": "TFLOP/s", "frac": k["frac_of_peak"], "traffic": traffic,
+                    "algorithmic_flop_per_launch": kflops[dom]}
+
+    tokens = world * B * T * args.steps
+    tok_s = tokens / dt
+    fpt = flops_per_token(cfg, T)
+    out = {
+        "metric": METRIC,
+        "value": round(tok_s, 1),
+        "unit": "tokens/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (uniform random tokens, resident in HBM)",
+        "config": {"workload": f"GPT-2 {args.model} training step: fwd+loss+bwd+grad-allreduce+AdamW, "
+                               f"dropout {args.dropout}",
+                   "model": f"GPT-2 {args.model}", "global_batch": B * world, "seq_len": T,
+                   "parallelism": f"dp{world}"},
+        "mfu": round(tok_s * fpt / (world * PEAK_BF16_TFLOPS * 1e12), 4),
+        "flop_per_token": fpt,
+        "final_loss": round(final_loss, 4),
+        "roofline": roofline,
+        "kernels": kernels,
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline(seq_len=T)
+        except Exception as e:  # reported, never fatal to the GPU measurement
+            out["cpu_baseline"] = {"error": repr(e)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,160 @@
+"""ctypes binding of libgpt2mi.so (the C ABI in include/gpt2mi.h).
+
+This is the only route from Python to the GPU math. There is no fallback: if the library is
+missing or the device is not a GPU, calls raise. Tensors are passed as raw device pointers;
+launches go on torch's current HIP stream.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgpt2mi.so")
+
+_c_int, _c_float, _c_size, _c_u64, _p = ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_void_p
+
+# name -> argtypes (all return int status unless listed in _RESTYPES)
+_SIGS = {
+    "gpt2mi_last_error": [],
+    "gpt2mi_abi_version": [],
+    "gpt2mi_embed_fwd": [_p, _p, _p, _p, _c_int, _c_int, _c_int, _c_float, _c_u64, _p],
+    "gpt2mi_embed_bwd": [_p, _p, _p, _p, _c_int, _c_int, _c_int, _c_float, _c_u64, _p],
+    "gpt2mi_layernorm_fwd": [_p, _p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_float, _p],
+    "gpt2mi_layernorm_bwd": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_float, _c_u64, _c_int, _p],
+    "gpt2mi_colsum_bf16": [_p, _p, _c_int, _c_int, _c_int, _p],
+    "gpt2mi_gemm": [_c_int, _c_int, _c_int, _c_int, _c_int, _p, _c_int, _p, _c_int, _p, _c_int, _p, _p, _p, _c_int,
+                    _c_float, _p, _c_int, _c_int, _c_float, _c_u64, _p],
+    "gpt2mi_attn_fwd": [_p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_float, _c_u64, _p],
+    "gpt2mi_attn_bwd": [_p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_float, _c_u64, _p],
+    "gpt2mi_xent_fwd": [_p, _c_int, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _p, _p, _p],
+    "gpt2mi_adamw": [_p, _p, _p, _p, _p, _c_size, _c_float, _c_float, _c_float, _c_float, _c_float, _c_int,
+                     _c_float, _p, _p, _p],
+    "gpt2mi_grad_norm": [_p, _c_size, _c_float, _p, _p, _p],
+    "gpt2mi_norm_partials_size": [],
+    "gpt2mi_cast_f32_bf16": [_p, _p, _c_size, _p],
+    "gpt2mi_scale_mul": [_p, _p, _p, _p],
+    "gpt2mi_memset_zero": [_p, _c_size, _p],
+}
+_RESTYPES = {"gpt2mi_last_error": ctypes.c_char_p}
+
+EXPORTED = tuple(_SIGS)
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+class KernelError(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load (once) and type the library. Raises if it is missing: there is no CPU fallback."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise KernelError(f"{path} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+                          " (or make -C gpt_2_distributed_amd/csrc)")
+    lib = ctypes.CDLL(path)
+    for name, args in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = _RESTYPES.get(name, ctypes.c_int)
+    _lib = lib
+    return lib
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise KernelError("gpt2mi kernels take device tensors only (got a CPU tensor)")
+    return t.data_ptr()
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _call(name: str, *args):
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.gpt2mi_last_error().decode(errors="replace")
+        raise KernelError(f"{name} failed ({rc}): {msg}")
+
+
+# ---- typed wrappers ------------------------------------------------------------------------------
+EPI_BF16, EPI_F32, EPI_RESID, EPI_GELU, EPI_GELU_BWD, EPI_ATOMIC = range(6)
+FWD, DGRAD, WGRAD = 0, 1, 2
+
+
+def embed_fwd(idx, wte, wpe, x, B, T, C, p=0.0, seed=0):
+    _call("gpt2mi_embed_fwd", _ptr(idx), _ptr(wte), _ptr(wpe), _ptr(x), B, T, C, p, seed, _stream())
+
+
+def embed_bwd(idx, dres, dwte, dwpe, B, T, C, p=0.0, seed=0):
+    _call("gpt2mi_embed_bwd", _ptr(idx), _ptr(dres), _ptr(dwte), _ptr(dwpe), B, T, C, p, seed, _stream())
+
+
+def layernorm_fwd(x, w, b, y_bf16, y_f32, mean, rstd, M, C, eps):
+    _call("gpt2mi_layernorm_fwd", _ptr(x), _ptr(w), _ptr(b), _ptr(y_bf16), _ptr(y_f32), _ptr(mean), _ptr(rstd),
+          M, C, eps, _stream())
+
+
+def layernorm_bwd(x, w, mean, rstd, dy, dres, dw, db, out_bf16, dbias_out, M, C, p_out=0.0, seed_out=0,
+                  dres_init=False):
+    _call("gpt2mi_layernorm_bwd", _ptr(x), _ptr(w), _ptr(mean), _ptr(rstd), _ptr(dy), _ptr(dres), _ptr(dw),
+          _ptr(db), _ptr(out_bf16), _ptr(dbias_out), M, C, p_out, seed_out, int(dres_init), _stream())
+
+
+def colsum_bf16(g, db, M, N, ld):
+    _call("gpt2mi_colsum_bf16", _ptr(g), _ptr(db), M, N, ld, _stream())
+
+
+def gemm(layout, epilogue, M, N, K, A, lda, B, ldb, C, ldc, bias=None, resid=None, aux=None, ldaux=0,
+         alpha=1.0, alpha_dev=None, accumulate=False, splits=1, p_drop=0.0, seed=0):
+    _call("gpt2mi_gemm", layout, epilogue, M, N, K, _ptr(A), lda, _ptr(B), ldb, _ptr(C), ldc, _ptr(bias),
+          _ptr(resid), _ptr(aux), ldaux, alpha, _ptr(alpha_dev), int(accumulate), splits, p_drop, seed, _stream())
+
+
+def attn_fwd(qkv, out, lse, B, T, H, D, p_drop=0.0, seed=0):
+    _call("gpt2mi_attn_fwd", _ptr(qkv), _ptr(out), _ptr(lse), B, T, H, D, p_drop, seed, _stream())
+
+
+def attn_bwd(qkv, out, dout, lse, delta, dqkv, B, T, H, D, p_drop=0.0, seed=0):
+    _call("gpt2mi_attn_bwd", _ptr(qkv), _ptr(out), _ptr(dout), _ptr(lse), _ptr(delta), _ptr(dqkv), B, T, H, D,
+          p_drop, seed, _stream())
+
+
+def xent_fwd(logits, ld, labels, loss_rows, lse, dlogits, ldd, M, V, loss, inv_count, ignore_index=-100):
+    _call("gpt2mi_xent_fwd", _ptr(logits), ld, _ptr(labels), _ptr(loss_rows), _ptr(lse), _ptr(dlogits), ldd, M, V,
+          ignore_index, _ptr(loss), _ptr(inv_count), _stream())
+
+
+def adamw(p, g, m, v, p_bf16, n, lr, wd, b1, b2, eps, step, grad_scale, partials, grad_norm):
+    _call("gpt2mi_adamw", _ptr(p), _ptr(g), _ptr(m), _ptr(v), _ptr(p_bf16), n, lr, wd, b1, b2, eps, step,
+          grad_scale, _ptr(partials), _ptr(grad_norm), _stream())
+
+
+def grad_norm(g, n, scale, partials, out):
+    _call("gpt2mi_grad_norm", _ptr(g), n, scale, _ptr(partials), _ptr(out), _stream())
+
+
+def norm_partials_size() -> int:
+    return load().gpt2mi_norm_partials_size()
+
+
+def cast_f32_bf16(x, y, n):
+    _call("gpt2mi_cast_f32_bf16", _ptr(x), _ptr(y), n, _stream())
+
+
+def scale_mul(a, b, out):
+    _call("gpt2mi_scale_mul", _ptr(a), _ptr(b), _ptr(out), _stream())
+
+
+def zero_(t: torch.Tensor):
+    _call("gpt2mi_memset_zero", _ptr(t), t.numel() * t.element_size(), _stream())

@@ -1,0 +1,445 @@
+// Causal flash attention forward/backward for gfx950, head_dim 64, bf16 in/out, fp32 softmax.
+//
+// Replaces (model.py:124-155): the [B,H,T,T] bmm -> /sqrt(D) ->
+// masked_fill(tril==0,-1e4) -> softmax(fp32) -> dropout -> bmm chain and its backward, with no
+// T x T tensor and no mask buffer (causality from tile indices; -1e4 and -inf give the same fp32
+// softmax since no row is fully masked).
+//
+// Layout in HBM (no view/transpose copies): q,k,v are read straight out of the qkv GEMM output
+// [B*T, 3C] (cols [0,C)=q, [C,2C)=k, [2C,3C)=v, head h at h*64), y is written head-merged into
+// [B*T, C], dq/dk/dv into the same [B*T, 3C] layout so the qkv backward GEMMs consume them as-is.
+//
+// MFMA formulation (v_mfma_f32_16x16x32_bf16), "key on the lane" / "query on the lane":
+//   forward / dQ : S^T = K Q^T  -> lane l holds 16 keys of query l&15: softmax stats per lane;
+//                  O^T += V^T P^T with P^T taken from the S^T accumulators IN REGISTERS (the MFMA
+//                  k-index is permuted consistently on both operands), V^T by ds_read_b64_tr_b16.
+//   dK/dV        : S = Q K^T    -> lane holds 16 queries of key l&15; dV^T += dO^T P, dK^T += Q^T dS
+//                  with P/dS from registers and dO^T/Q^T by transposed LDS reads.
+// LDS tiles are [64 rows][64 bf16] (128-B rows), 16-B chunk c stored at c ^ (row & 6): conflict-
+// free for both the ds_read_b128 row reads and the permuted transposed reads.
+#include "common.h"
+
+namespace {
+
+constexpr int D = 64;
+constexpr int BQ = 64;  // queries per workgroup (16 per wave)
+constexpr int BKV = 64; // keys per tile
+constexpr int kThreads = 256;
+constexpr float kLog2e = 1.4426950408889634f;
+
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ int t_off(int row, int chunk) { return row * 128 + 16 * (chunk ^ (row & 6)); }
+
+// row read: lane gets tile[row0 + (l&15)][32kk + 8g + 0..7]
+__device__ __forceinline__ bf16x8 row_frag(const char* base, int row0, int kk, int lane) {
+  return *reinterpret_cast<const bf16x8*>(base + t_off(row0 + (lane & 15), 4 * kk + (lane >> 4)));
+}
+
+// permuted transposed read: lane (g=l>>4, i=l&15) gets, for j = 0..7,
+//   tile[16*(2kk + (j>>2)) + 4g + (j&3)][c0 + i]
+__device__ __forceinline__ bf16x8 tr_frag(const char* base, int kk, int c0, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int chunk = (c0 >> 3) + (p >> 1);
+  const int r1 = 32 * kk + 4 * g + q;
+  const int r2 = r1 + 16;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + t_off(r1, chunk) + 8 * (p & 1)));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + t_off(r2, chunk) + 8 * (p & 1)));
+  s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+// pack accumulator registers acc[2kk + (j>>2)][j&3] (j = 0..7) to a bf16 operand fragment
+__device__ __forceinline__ bf16x8 pack_perm(const f32x4* acc, int kk) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = f2bf(acc[2 * kk + (j >> 2)][j & 3]);
+  return r;
+}
+
+// 64 rows x 128 B tile from a strided global matrix: 2 x 16-B chunks per thread.
+__device__ __forceinline__ void tile_load(u32x4* r, const bf16* src, size_t ld) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int id = threadIdx.x + kThreads * i;
+    r[i] = *reinterpret_cast<const u32x4*>(src + (size_t)(id >> 3) * ld + 8 * (id & 7));
+  }
+}
+__device__ __forceinline__ void tile_store(char* base, const u32x4* r) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int id = threadIdx.x + kThreads * i;
+    *reinterpret_cast<u32x4*>(base + t_off(id >> 3, id & 7)) = r[i];
+  }
+}
+
+__device__ __forceinline__ uint64_t att_idx(int bh, int T, int q, int k) {
+  return ((uint64_t)bh * T + q) * T + k;
+}
+
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void attn_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
+                                                            float* __restrict__ lse, int T, int H, float scale,
+                                                            uint64_t seed, uint32_t thr, float inv_keep) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * BKV * 128];  // 2 stages x (K, V)
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
+  const int nqb = T / BQ;
+  const int qb = nqb - 1 - blockIdx.x;  // heavy (late) query blocks first
+  const int bh = blockIdx.y, b = bh / H, h = bh % H;
+  const int C = H * D;
+  const size_t ld = 3 * (size_t)C;
+  const bf16* base = qkv + (size_t)b * T * ld;
+  const int q = qb * BQ + 16 * w + (lane & 15);  // this lane's query
+
+  // Q fragments (B operand of S^T = K Q^T): lane holds Q[q][32kk + 8g + j]
+  bf16x8 qf[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+    qf[kk] = *reinterpret_cast<const bf16x8*>(base + (size_t)q * ld + h * D + 32 * kk + 8 * g);
+
+  const float sl2 = scale * kLog2e;
+  float m = -INFINITY, l = 0.f;
+  f32x4 o[4];
+#pragma unroll
+  for (int f = 0; f < 4; ++f) o[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  u32x4 rk[2], rv[2];
+  const bf16* kbase = base + C + h * D;
+  const bf16* vbase = base + 2 * C + h * D;
+  tile_load(rk, kbase, ld);
+  tile_load(rv, vbase, ld);
+  tile_store(smem, rk);
+  tile_store(smem + BKV * 128, rv);
+  __syncthreads();
+
+  for (int j = 0; j <= qb; ++j) {
+    const int cur = j & 1;
+    const char* Ks = smem + cur * 2 * BKV * 128;
+    const char* Vs = Ks + BKV * 128;
+    if (j < qb) {
+      tile_load(rk, kbase + (size_t)(j + 1) * BKV * ld, ld);
+      tile_load(rv, vbase + (size_t)(j + 1) * BKV * ld, ld);
+    }
+    // S^T tile: s[fi][r] = S[key = 16fi + 4g + r][q]
+    f32x4 s[4];
+#pragma unroll
+    for (int fi = 0; fi < 4; ++fi) {
+      s[fi] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) s[fi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag(Ks, 16 * fi, kk, lane), qf[kk], s[fi], 0, 0, 0);
+    }
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int fi = 0; fi < 4; ++fi)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float t = s[fi][r] * sl2;
+        if (j == qb && (16 * fi + 4 * g + r) > (q - j * BKV)) t = -INFINITY;
+        s[fi][r] = t;
+        tmax = fmaxf(tmax, t);
+      }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float mn = fmaxf(m, tmax);
+    const float corr = exp2f(m - mn);
+    float rs = 0.f;
+#pragma unroll
+    for (int fi = 0; fi < 4; ++fi)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = exp2f(s[fi][r] - mn);
+        rs += p;
+        float pd = p;
+        if (thr) pd = drop_keep(seed, att_idx(bh, T, q, j * BKV + 16 * fi + 4 * g + r), thr) ? p * inv_keep : 0.f;
+        s[fi][r] = pd;
+      }
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    l = l * corr + rs;
+    m = mn;
+#pragma unroll
+    for (int f = 0; f < 4; ++f)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[f][r] *= corr;
+    // O^T[d][q] += V^T[d][key] P^T[key][q]
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const bf16x8 pf = pack_perm(s, kk);
+#pragma unroll
+      for (int fd = 0; fd < 4; ++fd) o[fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag(Vs, kk, 16 * fd, lane), pf, o[fd], 0, 0, 0);
+    }
+    if (j < qb) {
+      char* nxt = smem + (cur ^ 1) * 2 * BKV * 128;
+      tile_store(nxt, rk);
+      tile_store(nxt + BKV * 128, rv);
+    }
+    __syncthreads();
+  }
+  // finalize: o[fd][r] = O^T[d = 16fd + 4g + r][q]
+  const float il = 1.f / l;
+  bf16* op = out + ((size_t)b * T + q) * C + h * D;
+#pragma unroll
+  for (int fd = 0; fd < 4; ++fd)
+    *reinterpret_cast<bf16x4*>(op + 16 * fd + 4 * g) =
+        bf16x4{f2bf(o[fd][0] * il), f2bf(o[fd][1] * il), f2bf(o[fd][2] * il), f2bf(o[fd][3] * il)};
+  if (g == 0) lse[(size_t)bh * T + q] = (m + log2f(l)) / kLog2e;  // natural-log LSE of scaled scores
+}
+
+// ---------------------------------------------------------------------------------------------
+// delta[bh][t] = sum_d dO[b,t,h,d] * O[b,t,h,d]
+__global__ __launch_bounds__(256) void attn_delta_kernel(const bf16* __restrict__ out, const bf16* __restrict__ dout,
+                                                         float* __restrict__ delta, int B, int T, int H) {
+  const int i = blockIdx.x * 256 + threadIdx.x;  // over B*T*H, (b,t) major
+  if (i >= B * T * H) return;
+  const int h = i % H, bt = i / H, b = bt / T, t = bt % T;
+  const size_t off = (size_t)bt * H * D + h * D;
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < D; c += 8) {
+    bf16x8 a = *reinterpret_cast<const bf16x8*>(out + off + c);
+    bf16x8 d = *reinterpret_cast<const bf16x8*>(dout + off + c);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += bf2f(a[j]) * bf2f(d[j]);
+  }
+  delta[((size_t)b * H + h) * T + t] = s;
+}
+
+// ---------------------------------------------------------------------------------------------
+// dQ: query-outer; recomputes P from the saved LSE. dS^T = P^T o (dP^T - delta), dQ^T += K^T dS^T.
+__global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
+                                                               const float* __restrict__ lse, const float* __restrict__ delta,
+                                                               bf16* __restrict__ dqkv, int T, int H, float scale,
+                                                               uint64_t seed, uint32_t thr, float inv_keep) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * BKV * 128];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
+  const int nqb = T / BQ;
+  const int qb = nqb - 1 - blockIdx.x;
+  const int bh = blockIdx.y, b = bh / H, h = bh % H;
+  const int C = H * D;
+  const size_t ld = 3 * (size_t)C;
+  const bf16* base = qkv + (size_t)b * T * ld;
+  const int q = qb * BQ + 16 * w + (lane & 15);
+  bf16x8 qf[2], df[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    qf[kk] = *reinterpret_cast<const bf16x8*>(base + (size_t)q * ld + h * D + 32 * kk + 8 * g);
+    df[kk] = *reinterpret_cast<const bf16x8*>(dout + ((size_t)b * T + q) * C + h * D + 32 * kk + 8 * g);
+  }
+  const float sl2 = scale * kLog2e;
+  const float lse2 = lse[(size_t)bh * T + q] * kLog2e;
+  const float dl = delta[(size_t)bh * T + q];
+  f32x4 dq[4];
+#pragma unroll
+  for (int f = 0; f < 4; ++f) dq[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  u32x4 rk[2], rv[2];
+  const bf16* kbase = base + C + h * D;
+  const bf16* vbase = base + 2 * C + h * D;
+  tile_load(rk, kbase, ld);
+  tile_load(rv, vbase, ld);
+  tile_store(smem, rk);
+  tile_store(smem + BKV * 128, rv);
+  __syncthreads();
+  for (int j = 0; j <= qb; ++j) {
+    const int cur = j & 1;
+    const char* Ks = smem + cur * 2 * BKV * 128;
+    const char* Vs = Ks + BKV * 128;
+    if (j < qb) {
+      tile_load(rk, kbase + (size_t)(j + 1) * BKV * ld, ld);
+      tile_load(rv, vbase + (size_t)(j + 1) * BKV * ld, ld);
+    }
+    f32x4 s[4], dp[4];
+#pragma unroll
+    for (int fi = 0; fi < 4; ++fi) {
+      s[fi] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dp[fi] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        s[fi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag(Ks, 16 * fi, kk, lane), qf[kk], s[fi], 0, 0, 0);
+        dp[fi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag(Vs, 16 * fi, kk, lane), df[kk], dp[fi], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int fi = 0; fi < 4; ++fi)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = j * BKV + 16 * fi + 4 * g + r;
+        float p = (key > q) ? 0.f : exp2f(s[fi][r] * sl2 - lse2);
+        float d = dp[fi][r];
+        if (thr) d = drop_keep(seed, att_idx(bh, T, q, key), thr) ? d * inv_keep : 0.f;
+        s[fi][r] = p * (d - dl);  // dS^T
+      }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const bf16x8 sf = pack_perm(s, kk);
+#pragma unroll
+      for (int fd = 0; fd < 4; ++fd) dq[fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag(Ks, kk, 16 * fd, lane), sf, dq[fd], 0, 0, 0);
+    }
+    if (j < qb) {
+      char* nxt = smem + (cur ^ 1) * 2 * BKV * 128;
+      tile_store(nxt, rk);
+      tile_store(nxt + BKV * 128, rv);
+    }
+    __syncthreads();
+  }
+  bf16* dp_out = dqkv + ((size_t)b * T + q) * ld + h * D;
+#pragma unroll
+  for (int fd = 0; fd < 4; ++fd)
+    *reinterpret_cast<bf16x4*>(dp_out + 16 * fd + 4 * g) = bf16x4{
+        f2bf(dq[fd][0] * scale), f2bf(dq[fd][1] * scale), f2bf(dq[fd][2] * scale), f2bf(dq[fd][3] * scale)};
+}
+
+// ---------------------------------------------------------------------------------------------
+// dK, dV: key-outer over query tiles >= the key block (causal).
+__global__ __launch_bounds__(kThreads) void attn_bwd_dkdv_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
+                                                                 const float* __restrict__ lse, const float* __restrict__ delta,
+                                                                 bf16* __restrict__ dqkv, int T, int H, float scale,
+                                                                 uint64_t seed, uint32_t thr, float inv_keep) {
+  constexpr int kTile = BQ * 128;
+  __shared__ __attribute__((aligned(16))) char smem[2 * (2 * kTile + 2 * BQ * 4)];  // 2 x (Q, dO, lse, delta)
+  constexpr int kStage = 2 * kTile + 2 * BQ * 4;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
+  const int nkb = T / BKV;
+  const int kb = blockIdx.x;  // key block; light-to-heavy order does not matter much here
+  const int bh = blockIdx.y, b = bh / H, h = bh % H;
+  const int C = H * D;
+  const size_t ld = 3 * (size_t)C;
+  const bf16* base = qkv + (size_t)b * T * ld;
+  const int key = kb * BKV + 16 * w + (lane & 15);
+  bf16x8 kf[2], vf[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    kf[kk] = *reinterpret_cast<const bf16x8*>(base + (size_t)key * ld + C + h * D + 32 * kk + 8 * g);
+    vf[kk] = *reinterpret_cast<const bf16x8*>(base + (size_t)key * ld + 2 * C + h * D + 32 * kk + 8 * g);
+  }
+  const float sl2 = scale * kLog2e;
+  f32x4 dk[4], dv[4];
+#pragma unroll
+  for (int f = 0; f < 4; ++f) {
+    dk[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+    dv[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const bf16* qbase = base + h * D;
+  const bf16* dbase = dout + (size_t)b * T * C + h * D;
+  const float* lrow = lse + (size_t)bh * T;
+  const float* drow = delta + (size_t)bh * T;
+
+  u32x4 rq[2], rd[2];
+  float rl = 0.f, rdl = 0.f;
+  auto gload = [&](int i) {
+    tile_load(rq, qbase + (size_t)i * BQ * ld, ld);
+    tile_load(rd, dbase + (size_t)i * BQ * C, C);
+    if (threadIdx.x < BQ) {
+      rl = lrow[i * BQ + threadIdx.x] * kLog2e;
+      rdl = drow[i * BQ + threadIdx.x];
+    }
+  };
+  auto sstore = [&](char* st) {
+    tile_store(st, rq);
+    tile_store(st + kTile, rd);
+    if (threadIdx.x < BQ) {
+      reinterpret_cast<float*>(st + 2 * kTile)[threadIdx.x] = rl;
+      reinterpret_cast<float*>(st + 2 * kTile + BQ * 4)[threadIdx.x] = rdl;
+    }
+  };
+  gload(kb);
+  sstore(smem);
+  __syncthreads();
+  for (int i = kb; i < nkb; ++i) {
+    const int cur = (i - kb) & 1;
+    const char* Qs = smem + cur * kStage;
+    const char* Ds = Qs + kTile;
+    const float* Ls = reinterpret_cast<const float*>(Qs + 2 * kTile);
+    const float* Dl = Ls + BQ;
+    if (i + 1 < nkb) gload(i + 1);
+    f32x4 s[4], dp[4];
+#pragma unroll
+    for (int fi = 0; fi < 4; ++fi) {
+      s[fi] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dp[fi] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        s[fi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag(Qs, 16 * fi, kk, lane), kf[kk], s[fi], 0, 0, 0);
+        dp[fi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag(Ds, 16 * fi, kk, lane), vf[kk], dp[fi], 0, 0, 0);
+      }
+    }
+    // s[fi][r] = S[q = 16fi + 4g + r][key]
+    f32x4 pd[4];
+#pragma unroll
+    for (int fi = 0; fi < 4; ++fi) {
+      const f32x4 l4 = *reinterpret_cast<const f32x4*>(Ls + 16 * fi + 4 * g);
+      const f32x4 d4 = *reinterpret_cast<const f32x4*>(Dl + 16 * fi + 4 * g);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qq = i * BQ + 16 * fi + 4 * g + r;
+        const float p = (qq < key) ? 0.f : exp2f(s[fi][r] * sl2 - l4[r]);
+        float pdv = p, d = dp[fi][r];
+        if (thr) {
+          const bool keep = drop_keep(seed, att_idx(bh, T, qq, key), thr);
+          pdv = keep ? p * inv_keep : 0.f;
+          d = keep ? d * inv_keep : 0.f;
+        }
+        pd[fi][r] = pdv;
+        s[fi][r] = p * (d - d4[r]);  // dS
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const bf16x8 pf = pack_perm(pd, kk);
+      const bf16x8 sf = pack_perm(s, kk);
+#pragma unroll
+      for (int fd = 0; fd < 4; ++fd) {
+        dv[fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag(Ds, kk, 16 * fd, lane), pf, dv[fd], 0, 0, 0);
+        dk[fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag(Qs, kk, 16 * fd, lane), sf, dk[fd], 0, 0, 0);
+      }
+    }
+    if (i + 1 < nkb) sstore(smem + (cur ^ 1) * kStage);
+    __syncthreads();
+  }
+  bf16* kout = dqkv + ((size_t)b * T + key) * ld + C + h * D;
+  bf16* vout = kout + C;
+#pragma unroll
+  for (int fd = 0; fd < 4; ++fd) {
+    *reinterpret_cast<bf16x4*>(kout + 16 * fd + 4 * g) = bf16x4{
+        f2bf(dk[fd][0] * scale), f2bf(dk[fd][1] * scale), f2bf(dk[fd][2] * scale), f2bf(dk[fd][3] * scale)};
+    *reinterpret_cast<bf16x4*>(vout + 16 * fd + 4 * g) =
+        bf16x4{f2bf(dv[fd][0]), f2bf(dv[fd][1]), f2bf(dv[fd][2]), f2bf(dv[fd][3])};
+  }
+}
+
+}  // namespace
+
+GPT2MI_EXPORT int gpt2mi_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int T, int H, int head_dim,
+                                  float p_drop, uint64_t seed, void* stream) {
+  GPT2MI_REQUIRE(head_dim == D, "attn_fwd: head_dim=%d (only 64 is built)", head_dim);
+  GPT2MI_REQUIRE(T % BQ == 0 && T > 0, "attn_fwd: T=%d must be a multiple of %d", T, BQ);
+  const float scale = 1.f / sqrtf((float)head_dim);
+  dim3 grid(T / BQ, B * H);
+  attn_fwd_kernel<<<grid, kThreads, 0, (hipStream_t)stream>>>((const bf16*)qkv, (bf16*)out, lse, T, H, scale, seed,
+                                                              drop_threshold(p_drop),
+                                                              p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f);
+  return gpt2mi::check_launch("attn_fwd");
+}
+
+GPT2MI_EXPORT int gpt2mi_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse,
+                                  float* delta, uint16_t* dqkv, int B, int T, int H, int head_dim, float p_drop,
+                                  uint64_t seed, void* stream) {
+  GPT2MI_REQUIRE(head_dim == D, "attn_bwd: head_dim=%d (only 64 is built)", head_dim);
+  GPT2MI_REQUIRE(T % BQ == 0 && T > 0, "attn_bwd: T=%d must be a multiple of %d", T, BQ);
+  hipStream_t s = (hipStream_t)stream;
+  const float scale = 1.f / sqrtf((float)head_dim);
+  const uint32_t thr = drop_threshold(p_drop);
+  const float ik = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+  attn_delta_kernel<<<(B * T * H + 255) / 256, 256, 0, s>>>((const bf16*)out, (const bf16*)dout, delta, B, T, H);
+  int rc = gpt2mi::check_launch("attn_delta");
+  if (rc) return rc;
+  dim3 grid(T / BQ, B * H);
+  attn_bwd_dkdv_kernel<<<grid, kThreads, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta, (bf16*)dqkv, T, H,
+                                                 scale, seed, thr, ik);
+  rc = gpt2mi::check_launch("attn_bwd_dkdv");
+  if (rc) return rc;
+  attn_bwd_dq_kernel<<<grid, kThreads, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta, (bf16*)dqkv, T, H,
+                                               scale, seed, thr, ik);
+  return gpt2mi::check_launch("attn_bwd_dq");
+}

@@ -1,0 +1,76 @@
+// Shared device/host helpers for the gfx950 (MI355X, CDNA4) kernels of libgpt2mi.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+#define GPT2MI_EXPORT extern "C" __attribute__((visibility("default")))
+
+// ---- error reporting (C ABI: every entry returns 0 on success) ------------------------------
+namespace gpt2mi {
+void set_error(const char* fmt, ...);
+int check_launch(const char* what);
+}  // namespace gpt2mi
+
+#define GPT2MI_REQUIRE(cond, ...)                  \
+  do {                                             \
+    if (!(cond)) {                                 \
+      gpt2mi::set_error(__VA_ARGS__);              \
+      return 22; /* EINVAL */                      \
+    }                                              \
+  } while (0)
+
+// ---- bf16 helpers -----------------------------------------------------------------------------
+__device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
+__device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }  // RNE; v_cvt_pk_bf16_f32 on gfx950
+
+__device__ __forceinline__ float u16_to_f(uint16_t u) { return __uint_as_float(((uint32_t)u) << 16); }
+
+// ---- wave (64-lane) reductions ------------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ---- counter-based dropout RNG -------------------------------------------------------------------
+// keep(i) is a pure function of (seed, site offset, element index), so backward regenerates the
+// forward mask without storing it. 64-bit splitmix finaliser; 24 random bits compared to p*2^24.
+__device__ __forceinline__ uint32_t drop_bits(uint64_t seed, uint64_t idx) {
+  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (idx + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (uint32_t)(z >> 40);
+}
+// threshold = (uint32)(p * 2^24); keep if bits >= threshold.
+__device__ __forceinline__ bool drop_keep(uint64_t seed, uint64_t idx, uint32_t thr) {
+  return drop_bits(seed, idx) >= thr;
+}
+
+static inline uint32_t drop_threshold(float p) {
+  if (p <= 0.f) return 0u;
+  double t = (double)p * 16777216.0;
+  return (uint32_t)(t > 16777216.0 ? 16777216.0 : t);
+}
+
+// ---- XCD-aware block remap (blocks b and b+8 share an XCD; give each XCD a contiguous range) ----
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg / 8, r = nwg % 8;
+  const int xcd = bid % 8, idx = bid / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}

@@ -1,0 +1,334 @@
+// bf16 MFMA GEMM for gfx950 with fused epilogues — every Linear of the GPT-2 step.
+//
+//   C[m,n] (op)= epilogue( alpha * sum_k A(m,k) * B(n,k) )
+//
+// Operand layouts (template):
+//   A_T=0: A stored [M][K] (row m, k contiguous)     A_T=1: A stored [K][M] (m contiguous)
+//   B_T=0: B stored [N][K] (nn.Linear weight [out][in]) B_T=1: B stored [K][N]
+// forward (x @ W^T)       : A_T=0, B_T=0   (model.py:95-96,174-177,326 under autocast bf16)
+// dgrad   (dY @ W)        : A_T=0, B_T=1
+// wgrad   (dY^T @ X)      : A_T=1, B_T=1   (split-K over tokens, fp32 atomics into the grad arena)
+//
+// Structure: 256 threads = 4 waves (2x2), 128x128 block tile, BK=64, v_mfma_f32_16x16x32_bf16,
+// register-staged global->LDS double buffer (next tile's loads issued before the MFMAs, written
+// after them, one barrier per K-tile). LDS images:
+//   k-contiguous operand : [rows][64] bf16 (128-B rows), 16-B chunk c stored at c ^ (row & 7)
+//                          -> fragment reads are conflict-free ds_read_b128;
+//   m-contiguous operand : [64 k][128] bf16 (256-B rows), chunk c stored at c ^ 2*((k&3)|((k>>3&1)<<2))
+//                          -> fragments by two conflict-free ds_read_b64_tr_b16 (hardware transpose).
+// Epilogue: accumulators -> LDS (fp32, padded rows) -> row-contiguous 16-B chunks -> fused op -> HBM.
+#include "common.h"
+
+namespace {
+
+enum Epi : int {
+  EPI_BF16 = 0,      // C_bf16 = alpha*acc (+bias)
+  EPI_F32 = 1,       // C_f32 (+)= alpha*acc (+bias)           (beta = accumulate flag)
+  EPI_RESID = 2,     // C_f32 = resid_f32 + drop(alpha*acc + bias)
+  EPI_GELU = 3,      // aux_bf16 = u = acc+bias ; C_bf16 = drop(gelu(u))
+  EPI_GELU_BWD = 4,  // C_bf16 = drop_mask(alpha*acc) * gelu'(aux_bf16)
+  EPI_ATOMIC = 5,    // atomicAdd(C_f32, alpha*acc)            (split-K / accumulation)
+};
+
+constexpr int BM = 128, BN = 128, BK = 64;
+constexpr int kThreads = 256;
+constexpr int kStageBytes = (BM + BN) * BK * 2;           // 32 KiB
+constexpr int kEpiLd = BN + 4;                            // fp32 epilogue row stride (floats)
+constexpr int kLdsBytes = (2 * kStageBytes > BM * kEpiLd * 4) ? 2 * kStageBytes : BM * kEpiLd * 4;
+
+struct GemmParams {
+  const bf16* A;
+  const bf16* B;
+  void* C;
+  const float* bias;
+  const float* resid;
+  bf16* aux;  // EPI_GELU: pre-activation out; EPI_GELU_BWD: pre-activation in
+  const float* alpha_dev;
+  int M, N, K, lda, ldb, ldc, ldaux;
+  int k_per_split;
+  float alpha;
+  int accumulate;
+  uint64_t seed;
+  uint32_t thr;
+  float inv_keep;
+};
+
+__device__ __forceinline__ int kc_off(int row, int chunk) { return row * 128 + 16 * (chunk ^ (row & 7)); }
+__device__ __forceinline__ int mc_swz(int k) { return 2 * ((k & 3) | (((k >> 3) & 1) << 2)); }
+__device__ __forceinline__ int mc_off(int k, int chunk) { return k * 256 + 16 * ((chunk ^ mc_swz(k)) & 15); }
+
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+__device__ __forceinline__ bf16x8 read_frag_kc(const char* base, int row, int chunk) {
+  return *reinterpret_cast<const bf16x8*>(base + kc_off(row, chunk));
+}
+
+// tr read of the m-contiguous image: lane (g=l>>4, q=(l&15)>>2, p=l&3) gives A[m0+(l&15)][k0+8g+j]
+__device__ __forceinline__ bf16x8 read_frag_mc(const char* base, int k0, int m0, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int k1 = k0 + 8 * g + q;
+  const int chunk = (m0 >> 3) + (p >> 1);
+  const int off1 = mc_off(k1, chunk) + 8 * (p & 1);
+  const int off2 = mc_off(k1 + 4, chunk) + 8 * (p & 1);
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + off1));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + off2));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+__device__ __forceinline__ float gelu_f(float u) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float z = k0 * (u + k1 * u * u * u);
+  const float t = 1.f - 2.f / (__expf(2.f * z) + 1.f);  // tanh(z)
+  return 0.5f * u * (1.f + t);
+}
+__device__ __forceinline__ float gelu_grad_f(float u) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float z = k0 * (u + k1 * u * u * u);
+  const float t = 1.f - 2.f / (__expf(2.f * z) + 1.f);
+  return 0.5f * (1.f + t) + 0.5f * u * (1.f - t * t) * k0 * (1.f + 3.f * k1 * u * u);
+}
+
+// Tile loader: 4 x 16-B chunks per thread per operand per K-tile.
+template <bool TRANS, int ROWS>
+struct Loader {
+  // TRANS=0: tile is [ROWS][BK] from src[row*ld + k]; TRANS=1: tile is [BK][ROWS] from src[k*ld + row]
+  __device__ __forceinline__ static void load(u32x4* r, const bf16* src, int ld, int row0, int k0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int id = threadIdx.x + kThreads * i;
+      const bf16* p;
+      if constexpr (!TRANS) {
+        p = src + (size_t)(row0 + id / 8) * ld + k0 + 8 * (id % 8);
+      } else {
+        p = src + (size_t)(k0 + id / (ROWS / 8)) * ld + row0 + 8 * (id % (ROWS / 8));
+      }
+      r[i] = *reinterpret_cast<const u32x4*>(p);
+    }
+  }
+  __device__ __forceinline__ static void store(char* base, const u32x4* r) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int id = threadIdx.x + kThreads * i;
+      int off;
+      if constexpr (!TRANS) {
+        off = kc_off(id / 8, id % 8);
+      } else {
+        off = mc_off(id / (ROWS / 8), id % (ROWS / 8));
+      }
+      *reinterpret_cast<u32x4*>(base + off) = r[i];
+    }
+  }
+};
+
+template <bool A_T, bool B_T, int EPI>
+__global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams P) {
+  __shared__ __attribute__((aligned(16))) char smem[kLdsBytes];
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+
+  // tile scheduling: XCD-contiguous ranges, grouped-M ordering for L2 reuse
+  const int tiles_m = P.M / BM, tiles_n = P.N / BN;
+  const int ntiles = tiles_m * tiles_n;
+  const int pid = xcd_remap(blockIdx.x, ntiles);
+  constexpr int GM = 8;
+  const int group = pid / (GM * tiles_n);
+  const int first_m = group * GM;
+  const int gsz = min(tiles_m - first_m, GM);
+  const int tm = first_m + (pid % (GM * tiles_n)) % gsz;
+  const int tn = (pid % (GM * tiles_n)) / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kbeg = blockIdx.z * P.k_per_split;
+  const int nk = P.k_per_split / BK;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  u32x4 ra[4], rb[4];
+  using LA = Loader<A_T, BM>;
+  using LB = Loader<B_T, BN>;
+  LA::load(ra, P.A, P.lda, m0, kbeg);
+  LB::load(rb, P.B, P.ldb, n0, kbeg);
+  LA::store(smem, ra);
+  LB::store(smem + BM * BK * 2, rb);
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const char* As = smem + cur * kStageBytes;
+    const char* Bs = As + BM * BK * 2;
+    if (kt + 1 < nk) {
+      LA::load(ra, P.A, P.lda, m0, kbeg + (kt + 1) * BK);
+      LB::load(rb, P.B, P.ldb, n0, kbeg + (kt + 1) * BK);
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        if constexpr (!A_T) af[f] = read_frag_kc(As, wm * 64 + 16 * f + (lane & 15), 4 * kk + (lane >> 4));
+        else af[f] = read_frag_mc(As, 32 * kk, wm * 64 + 16 * f, lane);
+        if constexpr (!B_T) bfr[f] = read_frag_kc(Bs, wn * 64 + 16 * f + (lane & 15), 4 * kk + (lane >> 4));
+        else bfr[f] = read_frag_mc(Bs, 32 * kk, wn * 64 + 16 * f, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) {
+      char* nxt = smem + (cur ^ 1) * kStageBytes;
+      LA::store(nxt, ra);
+      LB::store(nxt + BM * BK * 2, rb);
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: accumulators -> LDS fp32 [BM][kEpiLd] ----
+  float* ep = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * 64 + 16 * i + 4 * (lane >> 4) + r;
+        const int col = wn * 64 + 16 * j + (lane & 15);
+        ep[row * kEpiLd + col] = acc[i][j][r];
+      }
+  __syncthreads();
+
+  float alpha = P.alpha;
+  if (P.alpha_dev) alpha *= P.alpha_dev[0];
+
+  if constexpr (EPI == EPI_ATOMIC) {
+    float* C = reinterpret_cast<float*>(P.C);
+#pragma unroll 4
+    for (int it = 0; it < (BM * BN) / kThreads; ++it) {
+      const int id = threadIdx.x + kThreads * it;
+      const int row = id / BN, col = id % BN;
+      atomicAdd(C + (size_t)(m0 + row) * P.ldc + n0 + col, alpha * ep[row * kEpiLd + col]);
+    }
+    return;
+  } else {
+#pragma unroll 2
+    for (int it = 0; it < (BM * BN) / (4 * kThreads); ++it) {
+      const int id = threadIdx.x + kThreads * it;
+      const int row = id / (BN / 4), c4 = 4 * (id % (BN / 4));
+      const int gm = m0 + row, gn = n0 + c4;
+      f32x4 v = *reinterpret_cast<const f32x4*>(ep + row * kEpiLd + c4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] *= alpha;
+      if (P.bias && EPI != EPI_GELU_BWD) {
+        f32x4 b = *reinterpret_cast<const f32x4*>(P.bias + gn);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] += b[j];
+      }
+      const size_t cidx = (size_t)gm * P.ldc + gn;
+      const uint64_t didx = (uint64_t)gm * P.N + gn;  // dropout element index in the logical [M,N]
+      if constexpr (EPI == EPI_BF16) {
+        bf16* C = reinterpret_cast<bf16*>(P.C);
+        *reinterpret_cast<bf16x4*>(C + cidx) = bf16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+      } else if constexpr (EPI == EPI_F32) {
+        float* C = reinterpret_cast<float*>(P.C);
+        if (P.accumulate) {
+          f32x4 o = *reinterpret_cast<const f32x4*>(C + cidx);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] += o[j];
+        }
+        *reinterpret_cast<f32x4*>(C + cidx) = v;
+      } else if constexpr (EPI == EPI_RESID) {
+        float* C = reinterpret_cast<float*>(P.C);
+        f32x4 r = *reinterpret_cast<const f32x4*>(P.resid + cidx);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float y = v[j];
+          if (P.thr) y = drop_keep(P.seed, didx + j, P.thr) ? y * P.inv_keep : 0.f;
+          r[j] += y;
+        }
+        *reinterpret_cast<f32x4*>(C + cidx) = r;
+      } else if constexpr (EPI == EPI_GELU) {
+        bf16* C = reinterpret_cast<bf16*>(P.C);
+        bf16x4 u, h;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          u[j] = f2bf(v[j]);
+          float a = gelu_f(v[j]);
+          if (P.thr) a = drop_keep(P.seed, didx + j, P.thr) ? a * P.inv_keep : 0.f;
+          h[j] = f2bf(a);
+        }
+        *reinterpret_cast<bf16x4*>(P.aux + (size_t)gm * P.ldaux + gn) = u;
+        *reinterpret_cast<bf16x4*>(C + cidx) = h;
+      } else if constexpr (EPI == EPI_GELU_BWD) {
+        bf16* C = reinterpret_cast<bf16*>(P.C);
+        bf16x4 u = *reinterpret_cast<const bf16x4*>(P.aux + (size_t)gm * P.ldaux + gn);
+        bf16x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float d = v[j];
+          if (P.thr) d = drop_keep(P.seed, didx + j, P.thr) ? d * P.inv_keep : 0.f;
+          o[j] = f2bf(d * gelu_grad_f(bf2f(u[j])));
+        }
+        *reinterpret_cast<bf16x4*>(C + cidx) = o;
+      }
+    }
+  }
+}
+
+template <bool A_T, bool B_T, int EPI>
+int launch(const GemmParams& P, int splits, hipStream_t s) {
+  dim3 grid((P.M / BM) * (P.N / BN), 1, splits);
+  gemm_kernel<A_T, B_T, EPI><<<grid, kThreads, 0, s>>>(P);
+  return gpt2mi::check_launch("gemm");
+}
+
+}  // namespace
+
+// layout: 0 = forward (A[M][K], B[N][K]); 1 = dgrad (A[M][K], B[K][N]); 2 = wgrad (A[K][M], B[K][N]).
+GPT2MI_EXPORT int gpt2mi_gemm(int layout, int epilogue, int M, int N, int K, const uint16_t* A, int lda,
+                              const uint16_t* B, int ldb, void* C, int ldc, const float* bias, const float* resid,
+                              uint16_t* aux, int ldaux, float alpha, const float* alpha_dev, int accumulate,
+                              int splits, float p_drop, uint64_t seed, void* stream) {
+  GPT2MI_REQUIRE(M % BM == 0 && N % BN == 0, "gemm: M=%d N=%d must be multiples of %d", M, N, BM);
+  GPT2MI_REQUIRE(splits >= 1 && K % (BK * splits) == 0, "gemm: K=%d must be a multiple of %d*splits(%d)", K, BK,
+                 splits);
+  GPT2MI_REQUIRE(splits == 1 || epilogue == EPI_ATOMIC, "gemm: split-K needs the atomic epilogue");
+  GPT2MI_REQUIRE(layout >= 0 && layout <= 2, "gemm: bad layout %d", layout);
+  GPT2MI_REQUIRE(ldc % 4 == 0 && (ldaux % 4 == 0 || aux == nullptr), "gemm: ldc/ldaux must be multiples of 4");
+  GemmParams P;
+  P.A = (const bf16*)A;
+  P.B = (const bf16*)B;
+  P.C = C;
+  P.bias = bias;
+  P.resid = resid;
+  P.aux = (bf16*)aux;
+  P.alpha_dev = alpha_dev;
+  P.M = M; P.N = N; P.K = K;
+  P.lda = lda; P.ldb = ldb; P.ldc = ldc; P.ldaux = ldaux;
+  P.k_per_split = K / splits;
+  P.alpha = alpha;
+  P.accumulate = accumulate;
+  P.seed = seed;
+  P.thr = drop_threshold(p_drop);
+  P.inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+  hipStream_t s = (hipStream_t)stream;
+  switch (layout * 16 + epilogue) {
+    case 0 * 16 + EPI_BF16: return launch<false, false, EPI_BF16>(P, splits, s);
+    case 0 * 16 + EPI_F32: return launch<false, false, EPI_F32>(P, splits, s);
+    case 0 * 16 + EPI_RESID: return launch<false, false, EPI_RESID>(P, splits, s);
+    case 0 * 16 + EPI_GELU: return launch<false, false, EPI_GELU>(P, splits, s);
+    case 1 * 16 + EPI_BF16: return launch<false, true, EPI_BF16>(P, splits, s);
+    case 1 * 16 + EPI_F32: return launch<false, true, EPI_F32>(P, splits, s);
+    case 1 * 16 + EPI_GELU_BWD: return launch<false, true, EPI_GELU_BWD>(P, splits, s);
+    case 2 * 16 + EPI_F32: return launch<true, true, EPI_F32>(P, splits, s);
+    case 2 * 16 + EPI_ATOMIC: return launch<true, true, EPI_ATOMIC>(P, splits, s);
+    default:
+      gpt2mi::set_error("gemm: unsupported layout %d / epilogue %d combination", layout, epilogue);
+      return 22;
+  }
+}

@@ -1,0 +1,259 @@
+// Fused softmax cross-entropy (loss + dlogits in one kernel), flat-arena fused AdamW with the
+// clip_grad_norm_(inf) sum of squares folded in and the bf16 weight shadow emitted, and helpers.
+//
+// Replaces: K13 log_softmax+nll_loss fwd/bwd (model.py:357-359), K15
+// clip_grad_norm_ (train_gpt2_distributed.py:419-421), K16 _fused_adamw_ (:356-362,424).
+#include "common.h"
+
+namespace {
+
+// --- cross entropy ------------------------------------------------------------------------------
+// One 256-thread block per row of logits (bf16, row stride ld, V valid columns).
+//   pass 1: online (max, sum exp) per thread over 16-B chunks, block combine -> lse
+//   loss_row = lse - logit[label]  (0 and not counted when label == ignore_index)
+//   pass 2: dlogits = softmax - onehot (bf16, unscaled; the 1/N and upstream grad are applied as
+//           the alpha of the backward GEMMs), zero in the padded columns [V, ld_d).
+__global__ __launch_bounds__(256) void xent_fwd_kernel(const bf16* __restrict__ logits, int ld,
+                                                       const int64_t* __restrict__ labels, float* __restrict__ loss_rows,
+                                                       float* __restrict__ lse_out, bf16* __restrict__ dlogits, int ldd,
+                                                       int V, int ignore_index) {
+  const int row = blockIdx.x;
+  const bf16* lp = logits + (size_t)row * ld;
+  const int tid = threadIdx.x;
+  float m = -INFINITY, s = 0.f;
+  for (int c = 8 * tid; c < V; c += 8 * 256) {
+    bf16x8 v = *reinterpret_cast<const bf16x8*>(lp + c);
+    float f[8];
+    float cm = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      f[j] = (c + j < V) ? bf2f(v[j]) : -INFINITY;
+      cm = fmaxf(cm, f[j]);
+    }
+    const float nm = fmaxf(m, cm);
+    float cs = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) cs += __expf(f[j] - nm);
+    s = s * __expf(m - nm) + cs;
+    m = nm;
+  }
+  // wave combine
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(m, o, 64), os = __shfl_xor(s, o, 64);
+    const float nm = fmaxf(m, om);
+    s = (m == -INFINITY ? 0.f : s * __expf(m - nm)) + (om == -INFINITY ? 0.f : os * __expf(om - nm));
+    m = nm;
+  }
+  __shared__ float sm[4], ss[4];
+  __shared__ float s_lse;
+  if ((tid & 63) == 0) {
+    sm[tid >> 6] = m;
+    ss[tid >> 6] = s;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float M_ = fmaxf(fmaxf(sm[0], sm[1]), fmaxf(sm[2], sm[3]));
+    float S_ = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) S_ += (sm[w] == -INFINITY) ? 0.f : ss[w] * __expf(sm[w] - M_);
+    const float lse = M_ + __logf(S_);
+    s_lse = lse;
+    lse_out[row] = lse;
+    const int64_t y = labels[row];
+    loss_rows[row] = (y == ignore_index) ? 0.f : lse - bf2f(lp[y]);
+  }
+  __syncthreads();
+  if (!dlogits) return;
+  const float lse = s_lse;
+  const int64_t y = labels[row];
+  bf16* dp = dlogits + (size_t)row * ldd;
+  const bool ign = (y == ignore_index);
+  for (int c = 8 * tid; c < ldd; c += 8 * 256) {
+    bf16x8 o;
+    if (c < V) {
+      bf16x8 v = *reinterpret_cast<const bf16x8*>(lp + c);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float d = (c + j < V && !ign) ? __expf(bf2f(v[j]) - lse) - ((c + j == y) ? 1.f : 0.f) : 0.f;
+        o[j] = f2bf(d);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(0.f);
+    }
+    *reinterpret_cast<bf16x8*>(dp + c) = o;
+  }
+}
+
+// loss = sum(loss_rows)/count(valid); inv_count = 1/count (the dlogits scale for backward).
+__global__ __launch_bounds__(1024) void xent_finalize_kernel(const float* __restrict__ loss_rows,
+                                                            const int64_t* __restrict__ labels, int M, int ignore_index,
+                                                            float* __restrict__ loss, float* __restrict__ inv_count) {
+  float s = 0.f, n = 0.f;
+  for (int i = threadIdx.x; i < M; i += 1024) {
+    s += loss_rows[i];
+    n += (labels[i] == ignore_index) ? 0.f : 1.f;
+  }
+  s = wave_sum(s);
+  n = wave_sum(n);
+  __shared__ float rs[16], rn[16];
+  if ((threadIdx.x & 63) == 0) {
+    rs[threadIdx.x >> 6] = s;
+    rn[threadIdx.x >> 6] = n;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float S = 0.f, N = 0.f;
+    for (int w = 0; w < 16; ++w) {
+      S += rs[w];
+      N += rn[w];
+    }
+    loss[0] = S / N;  // NaN when every label is ignored, as F.cross_entropy
+    inv_count[0] = 1.f / N;
+  }
+}
+
+// --- AdamW over the flat fp32 arena -------------------------------------------------------------
+// torch/optim/adam.py decoupled-decay math (train_gpt2_distributed.py:356-362):
+//   g *= grad_scale; p *= 1 - lr*wd; m = m + (1-b1)(g-m); v = b2 v + (1-b2) g^2;
+//   p -= step_size * m / (sqrt(v)/bc2_sqrt + eps)       step_size = lr/(1-b1^t), bc2_sqrt = sqrt(1-b2^t)
+// Also: partial sums of g^2 (the clip_grad_norm_(inf) total norm, computed from the same read of g
+// before the update, as the reference computes it before optim.step()), and the bf16 shadow of p.
+__global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                    float* __restrict__ m, float* __restrict__ v,
+                                                    bf16* __restrict__ pb, size_t n4, float lr, float wd, float b1,
+                                                    float b2, float eps, float step_size, float bc2_sqrt,
+                                                    float grad_scale, float* __restrict__ partials) {
+  float sq = 0.f;
+  const float decay = 1.f - lr * wd;
+  for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
+    f32x4 pv = reinterpret_cast<f32x4*>(p)[i];
+    f32x4 gv = reinterpret_cast<const f32x4*>(g)[i];
+    f32x4 mv = reinterpret_cast<f32x4*>(m)[i];
+    f32x4 vv = reinterpret_cast<f32x4*>(v)[i];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float gg = gv[j] * grad_scale;
+      sq += gg * gg;
+      float pp = pv[j] * decay;
+      const float mm = mv[j] + (1.f - b1) * (gg - mv[j]);
+      const float vvv = b2 * vv[j] + (1.f - b2) * gg * gg;
+      pp -= step_size * mm / (sqrtf(vvv) / bc2_sqrt + eps);
+      pv[j] = pp;
+      mv[j] = mm;
+      vv[j] = vvv;
+    }
+    reinterpret_cast<f32x4*>(p)[i] = pv;
+    reinterpret_cast<f32x4*>(m)[i] = mv;
+    reinterpret_cast<f32x4*>(v)[i] = vv;
+    if (pb) reinterpret_cast<bf16x4*>(pb)[i] = bf16x4{f2bf(pv[0]), f2bf(pv[1]), f2bf(pv[2]), f2bf(pv[3])};
+  }
+  sq = wave_sum(sq);
+  __shared__ float r[4];
+  if ((threadIdx.x & 63) == 0) r[threadIdx.x >> 6] = sq;
+  __syncthreads();
+  if (threadIdx.x == 0 && partials) partials[blockIdx.x] = r[0] + r[1] + r[2] + r[3];
+}
+
+__global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g, size_t n4, float scale,
+                                                    float* __restrict__ partials) {
+  float sq = 0.f;
+  for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
+    f32x4 gv = reinterpret_cast<const f32x4*>(g)[i];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sq += gv[j] * gv[j] * scale * scale;
+  }
+  sq = wave_sum(sq);
+  __shared__ float r[4];
+  if ((threadIdx.x & 63) == 0) r[threadIdx.x >> 6] = sq;
+  __syncthreads();
+  if (threadIdx.x == 0) partials[blockIdx.x] = r[0] + r[1] + r[2] + r[3];
+}
+
+// Deterministic final reduction of per-block partials: out = sqrt(sum).
+__global__ __launch_bounds__(256) void norm_finalize_kernel(const float* __restrict__ partials, int n,
+                                                            float* __restrict__ out) {
+  double s = 0.0;
+  for (int i = threadIdx.x; i < n; i += 256) s += partials[i];
+  __shared__ double r[256];
+  r[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) r[threadIdx.x] += r[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = (float)sqrt(r[0]);
+}
+
+__global__ __launch_bounds__(256) void cast_f32_bf16_kernel(const float* __restrict__ x, bf16* __restrict__ y, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) y[i] = f2bf(x[i]);
+}
+
+__global__ void scale_mul_kernel(const float* a, const float* b, float* out) { out[0] = a[0] * b[0]; }
+
+constexpr int kNormBlocks = 2048;
+
+}  // namespace
+
+GPT2MI_EXPORT int gpt2mi_xent_fwd(const uint16_t* logits, int ld, const int64_t* labels, float* loss_rows, float* lse,
+                                  uint16_t* dlogits, int ldd, int M, int V, int ignore_index, float* loss,
+                                  float* inv_count, void* stream) {
+  GPT2MI_REQUIRE(ld % 8 == 0 && ld >= V && (dlogits == nullptr || (ldd % 8 == 0 && ldd >= V)),
+                 "xent_fwd: row strides must be multiples of 8 and >= V (ld=%d ldd=%d V=%d)", ld, ldd, V);
+  hipStream_t s = (hipStream_t)stream;
+  xent_fwd_kernel<<<M, 256, 0, s>>>((const bf16*)logits, ld, labels, loss_rows, lse, (bf16*)dlogits, ldd, V,
+                                    ignore_index);
+  int rc = gpt2mi::check_launch("xent_fwd");
+  if (rc) return rc;
+  xent_finalize_kernel<<<1, 1024, 0, s>>>(loss_rows, labels, M, ignore_index, loss, inv_count);
+  return gpt2mi::check_launch("xent_finalize");
+}
+
+GPT2MI_EXPORT int gpt2mi_adamw(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, size_t n, float lr,
+                               float wd, float b1, float b2, float eps, int step, float grad_scale, float* partials,
+                               float* grad_norm, void* stream) {
+  GPT2MI_REQUIRE(n % 4 == 0, "adamw: n=%zu must be a multiple of 4", n);
+  GPT2MI_REQUIRE(step >= 1, "adamw: step must be >= 1");
+  hipStream_t s = (hipStream_t)stream;
+  const double bc1 = 1.0 - pow((double)b1, step), bc2 = 1.0 - pow((double)b2, step);
+  const float step_size = (float)(lr / bc1), bc2_sqrt = (float)sqrt(bc2);
+  adamw_kernel<<<kNormBlocks, 256, 0, s>>>(p, g, m, v, (bf16*)p_bf16, n / 4, lr, wd, b1, b2, eps, step_size, bc2_sqrt,
+                                           grad_scale, partials);
+  int rc = gpt2mi::check_launch("adamw");
+  if (rc || !grad_norm) return rc;
+  norm_finalize_kernel<<<1, 256, 0, s>>>(partials, kNormBlocks, grad_norm);
+  return gpt2mi::check_launch("adamw_norm");
+}
+
+GPT2MI_EXPORT int gpt2mi_grad_norm(const float* g, size_t n, float scale, float* partials, float* out, void* stream) {
+  GPT2MI_REQUIRE(n % 4 == 0, "grad_norm: n=%zu must be a multiple of 4", n);
+  hipStream_t s = (hipStream_t)stream;
+  sumsq_kernel<<<kNormBlocks, 256, 0, s>>>(g, n / 4, scale, partials);
+  int rc = gpt2mi::check_launch("grad_norm");
+  if (rc) return rc;
+  norm_finalize_kernel<<<1, 256, 0, s>>>(partials, kNormBlocks, out);
+  return gpt2mi::check_launch("grad_norm_finalize");
+}
+
+GPT2MI_EXPORT int gpt2mi_norm_partials_size(void) { return kNormBlocks; }
+
+GPT2MI_EXPORT int gpt2mi_cast_f32_bf16(const float* x, uint16_t* y, size_t n, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  cast_f32_bf16_kernel<<<2048, 256, 0, s>>>(x, (bf16*)y, n);
+  return gpt2mi::check_launch("cast_f32_bf16");
+}
+
+GPT2MI_EXPORT int gpt2mi_scale_mul(const float* a, const float* b, float* out, void* stream) {
+  scale_mul_kernel<<<1, 1, 0, (hipStream_t)stream>>>(a, b, out);
+  return gpt2mi::check_launch("scale_mul");
+}
+
+GPT2MI_EXPORT int gpt2mi_memset_zero(void* ptr, size_t bytes, void* stream) {
+  hipError_t e = hipMemsetAsync(ptr, 0, bytes, (hipStream_t)stream);
+  if (e != hipSuccess) {
+    gpt2mi::set_error("memset_zero: %s", hipGetErrorString(e));
+    return (int)e;
+  }
+  return 0;
+}

@@ -1,0 +1,97 @@
+/*
+ * gpt2mi.h — C ABI of libgpt2mi.so, the MI355X (gfx950) kernels of the GPT-2 training step.
+ *
+ * The reference (dpickem/gpt_2_distributed) has no native code and no FFI: its hot path is the
+ * implicit aten/cuBLAS/NCCL work behind model.py + train_gpt2_distributed.py. Each entry below
+ * replaces the aten work of the reference site cited next to it; the
+ * Python binding is gpt_2_distributed_amd/_lib.py (ctypes), see INTEGRATION.md.
+ *
+ * Conventions
+ *  - Every pointer is a DEVICE pointer allocated by the caller (PyTorch's caching allocator in
+ *    the package). Kernels never allocate or free.
+ *  - bf16 tensors are passed as uint16_t* (raw bf16 bits). Shapes are row-major with explicit
+ *    leading dimensions (in elements).
+ *  - `stream` is a hipStream_t passed as void*; all launches are asynchronous on it.
+ *  - Return value: 0 on success; otherwise an errno-style (22 = invalid argument) or hipError_t
+ *    code, with a message in gpt2mi_last_error() (thread-local).
+ *  - Dropout (p > 0) uses a counter-based hash of (seed, element index) so backward regenerates
+ *    the forward mask; p = 0 disables it.
+ */
+#ifndef GPT2MI_H
+#define GPT2MI_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+const char* gpt2mi_last_error(void);
+int gpt2mi_abi_version(void);
+
+/* K1: x[b,t,:] = drop(wte[idx[b,t],:] + wpe[t,:])  — model.py:295-304 (embedding, add, dropout). */
+int gpt2mi_embed_fwd(const int64_t* idx, const float* wte, const float* wpe, float* x, int B, int T, int C,
+                     float p, uint64_t seed, void* stream);
+/* embedding_dense_backward of both tables: dwte[idx] += g, dwpe[t] += sum_b g (g = dres masked). */
+int gpt2mi_embed_bwd(const int64_t* idx, const float* dres, float* dwte, float* dwpe, int B, int T, int C,
+                     float p, uint64_t seed, void* stream);
+
+/* K2: nn.LayerNorm forward — model.py:204,210,247 (used :215,218,311). y_bf16 and/or y_f32 may be NULL. */
+int gpt2mi_layernorm_fwd(const float* x, const float* w, const float* b, uint16_t* y_bf16, float* y_f32,
+                         float* mean, float* rstd, int M, int C, float eps, void* stream);
+/* native_layer_norm_backward fused with the residual gradient (dres += dx, or = dx if dres_init),
+ * dw/db += ; optionally emits out_bf16 = bf16(dres*keep/(1-p_out)) for the residual branch below and
+ * dbias_out += colsum(out_bf16) (that branch's bias grad). */
+int gpt2mi_layernorm_bwd(const float* x, const float* w, const float* mean, const float* rstd, const uint16_t* dy,
+                         float* dres, float* dw, float* db, uint16_t* out_bf16, float* dbias_out, int M, int C,
+                         float p_out, uint64_t seed_out, int dres_init, void* stream);
+
+/* Bias grad of an addmm: db[n] += sum_m g[m,n] (g bf16, row stride ld). */
+int gpt2mi_colsum_bf16(const uint16_t* g, float* db, int M, int N, int ld, void* stream);
+
+/* K3/K9/K10/K11/K12/K14 GEMMs — model.py:95-96,174-177,326 (nn.Linear under bf16 autocast) and their
+ * autograd backward (train_gpt2_distributed.py:412).
+ *   C[m,n] = epi(alpha*(alpha_dev?*alpha_dev:1) * sum_k A(m,k) B(n,k))
+ * layout 0: A[M][K], B[N][K]   (x @ W^T)        layout 1: A[M][K], B[K][N]   (dY @ W, dgrad)
+ * layout 2: A[K][M], B[K][N]   (dY^T @ X, wgrad)
+ * epilogue 0 BF16: C bf16 (+bias)            1 F32: C fp32 (+bias), += when accumulate
+ *          2 RESID: C fp32 = resid + drop(acc+bias)       3 GELU: aux = bf16(acc+bias), C = bf16(drop(gelu))
+ *          4 GELU_BWD: C = bf16(drop(acc) * gelu'(aux))    5 ATOMIC: C fp32 += acc (split-K over `splits`)
+ * Requires M, N multiples of 128 and K a multiple of 64*splits. */
+int gpt2mi_gemm(int layout, int epilogue, int M, int N, int K, const uint16_t* A, int lda, const uint16_t* B, int ldb,
+                void* C, int ldc, const float* bias, const float* resid, uint16_t* aux, int ldaux, float alpha,
+                const float* alpha_dev, int accumulate, int splits, float p_drop, uint64_t seed, void* stream);
+
+/* K4-K8: causal flash attention, head_dim 64 — model.py:124-155. q/k/v read from qkv [B*T, 3C];
+ * out [B*T, C] head-merged; lse [B*H, T] (natural log of the 1/sqrt(D)-scaled scores). */
+int gpt2mi_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int T, int H, int head_dim, float p_drop,
+                    uint64_t seed, void* stream);
+/* Backward: delta [B*H, T] workspace; dqkv [B*T, 3C] written in the qkv layout. */
+int gpt2mi_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse, float* delta,
+                    uint16_t* dqkv, int B, int T, int H, int head_dim, float p_drop, uint64_t seed, void* stream);
+
+/* K13: F.cross_entropy(logits.view(-1,V), labels.view(-1), ignore_index) — model.py:357-359.
+ * logits bf16 [M, ld]; writes loss_rows [M], lse [M], loss[0] = mean, inv_count[0] = 1/#valid and, if
+ * dlogits != NULL, dlogits = softmax - onehot (bf16 [M, ldd], unscaled, zero in columns >= V). */
+int gpt2mi_xent_fwd(const uint16_t* logits, int ld, const int64_t* labels, float* loss_rows, float* lse,
+                    uint16_t* dlogits, int ldd, int M, int V, int ignore_index, float* loss, float* inv_count,
+                    void* stream);
+
+/* K15+K16: fused AdamW over a flat fp32 arena (torch.optim.AdamW(lr, weight_decay, betas, eps), one
+ * param group, decoupled decay — train_gpt2_distributed.py:356-362,424) with g *= grad_scale, the
+ * clip_grad_norm_(inf) total norm of the scaled grads -> grad_norm[0] (partials: workspace of
+ * gpt2mi_norm_partials_size() floats), and the bf16 shadow p_bf16 (may be NULL). */
+int gpt2mi_adamw(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, size_t n, float lr, float wd,
+                 float b1, float b2, float eps, int step, float grad_scale, float* partials, float* grad_norm,
+                 void* stream);
+int gpt2mi_grad_norm(const float* g, size_t n, float scale, float* partials, float* out, void* stream);
+int gpt2mi_norm_partials_size(void);
+
+int gpt2mi_cast_f32_bf16(const float* x, uint16_t* y, size_t n, void* stream);
+int gpt2mi_scale_mul(const float* a, const float* b, float* out, void* stream);
+int gpt2mi_memset_zero(void* ptr, size_t bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GPT2MI_H */

@@ -1,0 +1,158 @@
+"""End-to-end parity of the HIP training step against the reference goldens (dropout 0).
+
+Tolerances (north star): bf16 loss within 2e-2 relative of the reference fp32 trajectory; per-op
+grads at bf16 GEMM resolution."""
+import json
+import os
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+
+from tests.conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+TINY = dict(n_layer=2, n_head=2, n_embd=128, vocab_size=509, n_positions=64, resid_pdrop=0.0, attn_pdrop=0.0)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def rel_err(a, b):
+    a, b = a.double(), b.double()
+    return float((a - b).norm() / (b.norm() + 1e-30))
+
+
+def _tiny_model():
+    from gpt_2_distributed_amd.model import GPT2, GPT2Config
+    return GPT2(GPT2Config(**TINY)).to(dev)
+
+
+def test_tiny_forward_backward_vs_reference_golden():
+    g = np.load(os.path.join(GOLDEN, "tiny_fwd_bwd.npz"))
+    m = _tiny_model()
+    idx = torch.from_numpy(g["idx"]).to(dev)
+    labels = torch.from_numpy(g["labels"]).to(dev)
+    logits, loss = m(idx, labels=labels)
+    assert logits.shape == (2, 64, 509) and logits.dtype == torch.bfloat16
+    assert rel_err(logits.float().cpu(), torch.from_numpy(g["logits"])) < 1e-2
+    assert abs(loss.item() - float(g["loss"])) / float(g["loss"]) < 2e-3
+    loss.backward()
+    for n, p in m.named_parameters():
+        ref = torch.from_numpy(g["grad:" + n])
+        e = rel_err(p.grad.cpu(), ref)
+        assert e < 3e-2, (n, e)
+
+
+def test_tiny_trajectory_vs_reference_golden():
+    ref = json.load(open(os.path.join(GOLDEN, "tiny_traj.json")))
+    m = _tiny_model()
+    opt = m.configure_optimizers(weight_decay=0.1, learning_rate=1e-4, betas=(0.9, 0.95))
+    rng = np.random.default_rng(99)
+    toks = (np.minimum(rng.zipf(1.2, size=(20, 4, 65)), 509) - 1).astype(np.int64)
+    losses, norms = [], []
+    for t in toks:
+        x = torch.from_numpy(t[:, :-1].copy()).to(dev)
+        y = torch.from_numpy(t[:, 1:].copy()).to(dev)
+        _, loss = m(x, labels=y)
+        loss.backward()
+        opt.step()
+        opt.zero_grad()
+        losses.append(loss.item())
+        norms.append(opt.grad_norm.item())
+    rl = np.abs(np.array(losses) - np.array(ref["losses"])) / np.array(ref["losses"])
+    assert rl.max() < 2e-2, rl
+    rn = np.abs(np.array(norms) - np.array(ref["grad_norms"])) / np.array(ref["grad_norms"])
+    assert rn.max() < 5e-2, rn
+
+
+def test_torch_optimizer_and_clip_grad_norm_interop():
+    """The reference trainer's own calls work on our parameters: torch AdamW + clip_grad_norm_(inf)
+    (the engine re-casts the bf16 shadow after a foreign in-place update)."""
+    g = np.load(os.path.join(GOLDEN, "tiny_fwd_bwd.npz"))
+    idx = torch.from_numpy(g["idx"]).to(dev)
+    labels = torch.from_numpy(g["labels"]).to(dev)
+    a, b = _tiny_model(), _tiny_model()
+    oa = torch.optim.AdamW(a.parameters(), lr=1e-3, weight_decay=0.1, betas=(0.9, 0.95))
+    ob = b.configure_optimizers(learning_rate=1e-3)
+    for _ in range(3):
+        _, la = a(idx, labels=labels)
+        la.backward()
+        na = torch.nn.utils.clip_grad_norm_(a.parameters(), float("inf"))
+        oa.step()
+        oa.zero_grad()
+        _, lb = b(idx, labels=labels)
+        lb.backward()
+        ob.step()
+        ob.zero_grad()
+        assert abs(na.item() - ob.grad_norm.item()) < 1e-4 * na.item()
+        assert abs(la.item() - lb.item()) < 1e-5 * la.item()
+    assert rel_err(a.arena.cpu(), b.arena.cpu()) < 1e-6
+
+
+def test_grad_accumulation_equals_big_batch():
+    g = np.load(os.path.join(GOLDEN, "tiny_fwd_bwd.npz"))
+    idx = torch.from_numpy(g["idx"]).to(dev)
+    labels = torch.from_numpy(g["labels"]).to(dev)
+    a, b = _tiny_model(), _tiny_model()
+    _, l = a(idx, labels=labels)
+    l.backward()
+    for i in range(2):
+        _, lb = b(idx[i:i + 1], labels=labels[i:i + 1])
+        (lb / 2).backward()
+    for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
+        assert rel_err(pb.grad.cpu(), pa.grad.cpu()) < 2e-2, n
+
+
+def test_dropout_train_vs_eval():
+    from gpt_2_distributed_amd.model import GPT2, GPT2Config
+    cfg = dict(TINY, resid_pdrop=0.1, attn_pdrop=0.1)
+    m = GPT2(GPT2Config(**cfg)).to(dev)
+    g = np.load(os.path.join(GOLDEN, "tiny_fwd_bwd.npz"))
+    idx = torch.from_numpy(g["idx"]).to(dev)
+    labels = torch.from_numpy(g["labels"]).to(dev)
+    m.eval()
+    with torch.no_grad():
+        _, l0 = m(idx, labels=labels)
+        _, l1 = m(idx, labels=labels)
+    assert l0.item() == l1.item()
+    assert abs(l0.item() - float(g["loss"])) / float(g["loss"]) < 2e-3  # eval == no dropout
+    m.train()
+    _, lt = m(idx, labels=labels)
+    lt.backward()
+    assert torch.isfinite(lt) and lt.item() != l0.item()
+    assert all(torch.isfinite(p.grad).all() for p in m.parameters())
+
+
+@pytest.mark.parametrize("steps", [20])
+def test_124m_bf16_trajectory_vs_reference(steps):
+    """124M, B=4, T=1024, Zipf shards, 2 workers: bf16 loss within 2e-2 of the reference's fp32
+    CPU trajectory at every step (tests/golden/traj_124m.json)."""
+    path = os.path.join(GOLDEN, "traj_124m.json")
+    if not os.path.exists(path):
+        pytest.skip("traj golden missing")
+    ref = json.load(open(path))
+    from gpt_2_distributed_amd import dataloader as D, synthetic
+    from gpt_2_distributed_amd.model import GPT2, GPT2Config
+    m = GPT2(GPT2Config(resid_pdrop=0.0, attn_pdrop=0.0)).to(dev)
+    opt = m.configure_optimizers(learning_rate=1e-4)
+    losses = []
+    with tempfile.TemporaryDirectory() as d:
+        synthetic.write_shards(d, 2, 200_000, dist="zipf", seed=1234)
+        it = D.iter_batches(D.get_shard_paths(d, "train"), 1024, 4, num_workers=2)
+        for _ in range(steps):
+            x, y = next(it)
+            _, loss = m(x.to(dev), labels=y.to(dev))
+            loss.backward()
+            opt.step()
+            opt.zero_grad()
+            losses.append(loss.item())
+    rl = np.abs(np.array(losses) - np.array(ref["losses"][:steps])) / np.array(ref["losses"][:steps])
+    print("max rel loss err", rl.max(), losses[0], losses[-1])
+    assert rl.max() < 2e-2, rl
