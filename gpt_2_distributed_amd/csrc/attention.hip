@@ -9,6 +9,10 @@
 // [B*T, 3C] (cols [0,C)=q, [C,2C)=k, [2C,3C)=v, head h at h*64), y is written head-merged into
 // [B*T, C], dq/dk/dv into the same [B*T, 3C] layout so the qkv backward GEMMs consume them as-is.
 //
+// Work split: a wave owns 32 queries (fwd, dQ) or 32 keys (dK/dV) as two 16-lane MFMA groups, so
+// every K/V (Q/dO) fragment read from LDS feeds two MFMAs; 4 waves per workgroup; heavy (late
+// query / early key) blocks are dispatched first for the causal imbalance; key tiles that are fully
+// masked for a wave are skipped wave-uniformly.
 // MFMA formulation (v_mfma_f32_16x16x32_bf16), "key on the lane" / "query on the lane":
 //   forward / dQ : S^T = K Q^T  -> lane l holds 16 keys of query l&15: softmax stats per lane;
 //                  O^T += V^T P^T with P^T taken from the S^T accumulators IN REGISTERS (the MFMA
@@ -22,8 +26,10 @@
 namespace {
 
 constexpr int D = 64;
-constexpr int BQ = 64;  // queries per workgroup (16 per wave)
-constexpr int BKV = 64; // keys per tile
+constexpr int BQ = 128;  // queries per workgroup in fwd / dQ (32 per wave = two 16-query MFMA groups)
+constexpr int BKV = 64;  // keys per K/V tile in fwd / dQ
+constexpr int BKB = 128; // keys per workgroup in dK/dV (32 per wave)
+constexpr int BQT = 64;  // queries per Q/dO tile in dK/dV
 constexpr int kThreads = 256;
 constexpr float kLog2e = 1.4426950408889634f;
 
@@ -79,9 +85,9 @@ __device__ __forceinline__ uint64_t att_idx(int bh, int T, int q, int k) {
 }
 
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kThreads) void attn_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
-                                                            float* __restrict__ lse, int T, int H, float scale,
-                                                            uint64_t seed, uint32_t thr, float inv_keep) {
+__global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
+                                                               float* __restrict__ lse, int T, int H, float scale,
+                                                               uint64_t seed, uint32_t thr, float inv_keep) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * BKV * 128];  // 2 stages x (K, V)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
   const int nqb = T / BQ;
@@ -90,100 +96,121 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(const bf16* __restri
   const int C = H * D;
   const size_t ld = 3 * (size_t)C;
   const bf16* base = qkv + (size_t)b * T * ld;
-  const int q = qb * BQ + 16 * w + (lane & 15);  // this lane's query
+  const int q_lo = qb * BQ + 32 * w;  // first query of this wave
 
-  // Q fragments (B operand of S^T = K Q^T): lane holds Q[q][32kk + 8g + j]
-  bf16x8 qf[2];
+  bf16x8 qf[2][2];
 #pragma unroll
-  for (int kk = 0; kk < 2; ++kk)
-    qf[kk] = *reinterpret_cast<const bf16x8*>(base + (size_t)q * ld + h * D + 32 * kk + 8 * g);
-
+  for (int qg = 0; qg < 2; ++qg)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+      qf[qg][kk] = *reinterpret_cast<const bf16x8*>(base + (size_t)(q_lo + 16 * qg + (lane & 15)) * ld + h * D +
+                                                    32 * kk + 8 * g);
   const float sl2 = scale * kLog2e;
-  float m = -INFINITY, l = 0.f;
-  f32x4 o[4];
+  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
+  f32x4 o[2][4];
 #pragma unroll
-  for (int f = 0; f < 4; ++f) o[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int qg = 0; qg < 2; ++qg)
+#pragma unroll
+    for (int f = 0; f < 4; ++f) o[qg][f] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   u32x4 rk[2], rv[2];
   const bf16* kbase = base + C + h * D;
   const bf16* vbase = base + 2 * C + h * D;
+  const int nkv = (qb + 1) * BQ / BKV;
   tile_load(rk, kbase, ld);
   tile_load(rv, vbase, ld);
   tile_store(smem, rk);
   tile_store(smem + BKV * 128, rv);
   __syncthreads();
 
-  for (int j = 0; j <= qb; ++j) {
+  for (int j = 0; j < nkv; ++j) {
     const int cur = j & 1;
     const char* Ks = smem + cur * 2 * BKV * 128;
     const char* Vs = Ks + BKV * 128;
-    if (j < qb) {
+    if (j + 1 < nkv) {
       tile_load(rk, kbase + (size_t)(j + 1) * BKV * ld, ld);
       tile_load(rv, vbase + (size_t)(j + 1) * BKV * ld, ld);
     }
-    // S^T tile: s[fi][r] = S[key = 16fi + 4g + r][q]
-    f32x4 s[4];
+    const int k_lo = j * BKV;
+    if (k_lo <= q_lo + 31) {  // wave-uniform: some key of the tile is visible to some query of the wave
+      const bool diag = k_lo + BKV - 1 > q_lo;
+      f32x4 s[2][4];
 #pragma unroll
-    for (int fi = 0; fi < 4; ++fi) {
-      s[fi] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int fi = 0; fi < 4; ++fi) {
+        s[0][fi] = s[1][fi] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) s[fi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag(Ks, 16 * fi, kk, lane), qf[kk], s[fi], 0, 0, 0);
-    }
-    float tmax = -INFINITY;
-#pragma unroll
-    for (int fi = 0; fi < 4; ++fi)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float t = s[fi][r] * sl2;
-        if (j == qb && (16 * fi + 4 * g + r) > (q - j * BKV)) t = -INFINITY;
-        s[fi][r] = t;
-        tmax = fmaxf(tmax, t);
+        for (int kk = 0; kk < 2; ++kk) {
+          const bf16x8 kf = row_frag(Ks, 16 * fi, kk, lane);
+          s[0][fi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[0][kk], s[0][fi], 0, 0, 0);
+          s[1][fi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[1][kk], s[1][fi], 0, 0, 0);
+        }
       }
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    const float mn = fmaxf(m, tmax);
-    const float corr = exp2f(m - mn);
-    float rs = 0.f;
 #pragma unroll
-    for (int fi = 0; fi < 4; ++fi)
+      for (int qg = 0; qg < 2; ++qg) {
+        const int q = q_lo + 16 * qg + (lane & 15);
+        float tmax = -INFINITY;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float p = exp2f(s[fi][r] - mn);
-        rs += p;
-        float pd = p;
-        if (thr) pd = drop_keep(seed, att_idx(bh, T, q, j * BKV + 16 * fi + 4 * g + r), thr) ? p * inv_keep : 0.f;
-        s[fi][r] = pd;
+        for (int fi = 0; fi < 4; ++fi)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float t = s[qg][fi][r] * sl2;
+            if (diag && (k_lo + 16 * fi + 4 * g + r) > q) t = -INFINITY;
+            s[qg][fi][r] = t;
+            tmax = fmaxf(tmax, t);
+          }
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+        const float mn = fmaxf(m[qg], tmax);  // finite: tile 0 holds key 0, visible to every query
+        const float corr = exp2f(m[qg] - mn);
+        float rs = 0.f;
+#pragma unroll
+        for (int fi = 0; fi < 4; ++fi)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float p = exp2f(s[qg][fi][r] - mn);
+            rs += p;
+            float pd = p;
+            if (thr) pd = drop_keep(seed, att_idx(bh, T, q, k_lo + 16 * fi + 4 * g + r), thr) ? p * inv_keep : 0.f;
+            s[qg][fi][r] = pd;
+          }
+        rs += __shfl_xor(rs, 16, 64);
+        rs += __shfl_xor(rs, 32, 64);
+        l[qg] = l[qg] * corr + rs;
+        m[qg] = mn;
+#pragma unroll
+        for (int f = 0; f < 4; ++f)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[qg][f][r] *= corr;
       }
-    rs += __shfl_xor(rs, 16, 64);
-    rs += __shfl_xor(rs, 32, 64);
-    l = l * corr + rs;
-    m = mn;
 #pragma unroll
-    for (int f = 0; f < 4; ++f)
+      for (int kk = 0; kk < 2; ++kk) {
+        const bf16x8 p0 = pack_perm(s[0], kk), p1 = pack_perm(s[1], kk);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) o[f][r] *= corr;
-    // O^T[d][q] += V^T[d][key] P^T[key][q]
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const bf16x8 pf = pack_perm(s, kk);
-#pragma unroll
-      for (int fd = 0; fd < 4; ++fd) o[fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag(Vs, kk, 16 * fd, lane), pf, o[fd], 0, 0, 0);
+        for (int fd = 0; fd < 4; ++fd) {
+          const bf16x8 vt = tr_frag(Vs, kk, 16 * fd, lane);
+          o[0][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vt, p0, o[0][fd], 0, 0, 0);
+          o[1][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vt, p1, o[1][fd], 0, 0, 0);
+        }
+      }
     }
-    if (j < qb) {
+    if (j + 1 < nkv) {
       char* nxt = smem + (cur ^ 1) * 2 * BKV * 128;
       tile_store(nxt, rk);
       tile_store(nxt + BKV * 128, rv);
     }
     __syncthreads();
   }
-  // finalize: o[fd][r] = O^T[d = 16fd + 4g + r][q]
-  const float il = 1.f / l;
-  bf16* op = out + ((size_t)b * T + q) * C + h * D;
 #pragma unroll
-  for (int fd = 0; fd < 4; ++fd)
-    *reinterpret_cast<bf16x4*>(op + 16 * fd + 4 * g) =
-        bf16x4{f2bf(o[fd][0] * il), f2bf(o[fd][1] * il), f2bf(o[fd][2] * il), f2bf(o[fd][3] * il)};
-  if (g == 0) lse[(size_t)bh * T + q] = (m + log2f(l)) / kLog2e;  // natural-log LSE of scaled scores
+  for (int qg = 0; qg < 2; ++qg) {
+    const int q = q_lo + 16 * qg + (lane & 15);
+    const float il = 1.f / l[qg];
+    bf16* op = out + ((size_t)b * T + q) * C + h * D;
+#pragma unroll
+    for (int fd = 0; fd < 4; ++fd)
+      *reinterpret_cast<bf16x4*>(op + 16 * fd + 4 * g) = bf16x4{f2bf(o[qg][fd][0] * il), f2bf(o[qg][fd][1] * il),
+                                                                f2bf(o[qg][fd][2] * il), f2bf(o[qg][fd][3] * il)};
+    if (g == 0) lse[(size_t)bh * T + q] = (m[qg] + log2f(l[qg])) / kLog2e;  // natural-log LSE of scaled scores
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -207,10 +234,12 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16* __restrict_
 
 // ---------------------------------------------------------------------------------------------
 // dQ: query-outer; recomputes P from the saved LSE. dS^T = P^T o (dP^T - delta), dQ^T += K^T dS^T.
-__global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
-                                                               const float* __restrict__ lse, const float* __restrict__ delta,
-                                                               bf16* __restrict__ dqkv, int T, int H, float scale,
-                                                               uint64_t seed, uint32_t thr, float inv_keep) {
+__global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const bf16* __restrict__ qkv,
+                                                                  const bf16* __restrict__ dout,
+                                                                  const float* __restrict__ lse,
+                                                                  const float* __restrict__ delta,
+                                                                  bf16* __restrict__ dqkv, int T, int H, float scale,
+                                                                  uint64_t seed, uint32_t thr, float inv_keep) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * BKV * 128];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
   const int nqb = T / BQ;
@@ -219,107 +248,140 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(const bf16* __res
   const int C = H * D;
   const size_t ld = 3 * (size_t)C;
   const bf16* base = qkv + (size_t)b * T * ld;
-  const int q = qb * BQ + 16 * w + (lane & 15);
-  bf16x8 qf[2], df[2];
+  const int q_lo = qb * BQ + 32 * w;
+  bf16x8 qf[2][2], df[2][2];
+  float lse2[2], dl[2];
 #pragma unroll
-  for (int kk = 0; kk < 2; ++kk) {
-    qf[kk] = *reinterpret_cast<const bf16x8*>(base + (size_t)q * ld + h * D + 32 * kk + 8 * g);
-    df[kk] = *reinterpret_cast<const bf16x8*>(dout + ((size_t)b * T + q) * C + h * D + 32 * kk + 8 * g);
+  for (int qg = 0; qg < 2; ++qg) {
+    const int q = q_lo + 16 * qg + (lane & 15);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      qf[qg][kk] = *reinterpret_cast<const bf16x8*>(base + (size_t)q * ld + h * D + 32 * kk + 8 * g);
+      df[qg][kk] = *reinterpret_cast<const bf16x8*>(dout + ((size_t)b * T + q) * C + h * D + 32 * kk + 8 * g);
+    }
+    lse2[qg] = lse[(size_t)bh * T + q] * kLog2e;
+    dl[qg] = delta[(size_t)bh * T + q];
   }
   const float sl2 = scale * kLog2e;
-  const float lse2 = lse[(size_t)bh * T + q] * kLog2e;
-  const float dl = delta[(size_t)bh * T + q];
-  f32x4 dq[4];
+  f32x4 dq[2][4];
 #pragma unroll
-  for (int f = 0; f < 4; ++f) dq[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int qg = 0; qg < 2; ++qg)
+#pragma unroll
+    for (int f = 0; f < 4; ++f) dq[qg][f] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   u32x4 rk[2], rv[2];
   const bf16* kbase = base + C + h * D;
   const bf16* vbase = base + 2 * C + h * D;
+  const int nkv = (qb + 1) * BQ / BKV;
   tile_load(rk, kbase, ld);
   tile_load(rv, vbase, ld);
   tile_store(smem, rk);
   tile_store(smem + BKV * 128, rv);
   __syncthreads();
-  for (int j = 0; j <= qb; ++j) {
+  for (int j = 0; j < nkv; ++j) {
     const int cur = j & 1;
     const char* Ks = smem + cur * 2 * BKV * 128;
     const char* Vs = Ks + BKV * 128;
-    if (j < qb) {
+    if (j + 1 < nkv) {
       tile_load(rk, kbase + (size_t)(j + 1) * BKV * ld, ld);
       tile_load(rv, vbase + (size_t)(j + 1) * BKV * ld, ld);
     }
-    f32x4 s[4], dp[4];
+    const int k_lo = j * BKV;
+    if (k_lo <= q_lo + 31) {
+      const bool diag = k_lo + BKV - 1 > q_lo;
+      f32x4 s[2][4], dp[2][4];
 #pragma unroll
-    for (int fi = 0; fi < 4; ++fi) {
-      s[fi] = f32x4{0.f, 0.f, 0.f, 0.f};
-      dp[fi] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int fi = 0; fi < 4; ++fi) {
+        s[0][fi] = s[1][fi] = dp[0][fi] = dp[1][fi] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          const bf16x8 kf = row_frag(Ks, 16 * fi, kk, lane);
+          const bf16x8 vf = row_frag(Vs, 16 * fi, kk, lane);
+#pragma unroll
+          for (int qg = 0; qg < 2; ++qg) {
+            s[qg][fi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qg][kk], s[qg][fi], 0, 0, 0);
+            dp[qg][fi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, df[qg][kk], dp[qg][fi], 0, 0, 0);
+          }
+        }
+      }
+#pragma unroll
+      for (int qg = 0; qg < 2; ++qg) {
+        const int q = q_lo + 16 * qg + (lane & 15);
+#pragma unroll
+        for (int fi = 0; fi < 4; ++fi)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = k_lo + 16 * fi + 4 * g + r;
+            const float p = (diag && key > q) ? 0.f : exp2f(s[qg][fi][r] * sl2 - lse2[qg]);
+            float d = dp[qg][fi][r];
+            if (thr) d = drop_keep(seed, att_idx(bh, T, q, key), thr) ? d * inv_keep : 0.f;
+            s[qg][fi][r] = p * (d - dl[qg]);  // dS^T
+          }
+      }
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
-        s[fi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag(Ks, 16 * fi, kk, lane), qf[kk], s[fi], 0, 0, 0);
-        dp[fi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag(Vs, 16 * fi, kk, lane), df[kk], dp[fi], 0, 0, 0);
+        const bf16x8 s0 = pack_perm(s[0], kk), s1 = pack_perm(s[1], kk);
+#pragma unroll
+        for (int fd = 0; fd < 4; ++fd) {
+          const bf16x8 kt = tr_frag(Ks, kk, 16 * fd, lane);
+          dq[0][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kt, s0, dq[0][fd], 0, 0, 0);
+          dq[1][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kt, s1, dq[1][fd], 0, 0, 0);
+        }
       }
     }
-#pragma unroll
-    for (int fi = 0; fi < 4; ++fi)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = j * BKV + 16 * fi + 4 * g + r;
-        float p = (key > q) ? 0.f : exp2f(s[fi][r] * sl2 - lse2);
-        float d = dp[fi][r];
-        if (thr) d = drop_keep(seed, att_idx(bh, T, q, key), thr) ? d * inv_keep : 0.f;
-        s[fi][r] = p * (d - dl);  // dS^T
-      }
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const bf16x8 sf = pack_perm(s, kk);
-#pragma unroll
-      for (int fd = 0; fd < 4; ++fd) dq[fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag(Ks, kk, 16 * fd, lane), sf, dq[fd], 0, 0, 0);
-    }
-    if (j < qb) {
+    if (j + 1 < nkv) {
       char* nxt = smem + (cur ^ 1) * 2 * BKV * 128;
       tile_store(nxt, rk);
       tile_store(nxt + BKV * 128, rv);
     }
     __syncthreads();
   }
-  bf16* dp_out = dqkv + ((size_t)b * T + q) * ld + h * D;
 #pragma unroll
-  for (int fd = 0; fd < 4; ++fd)
-    *reinterpret_cast<bf16x4*>(dp_out + 16 * fd + 4 * g) = bf16x4{
-        f2bf(dq[fd][0] * scale), f2bf(dq[fd][1] * scale), f2bf(dq[fd][2] * scale), f2bf(dq[fd][3] * scale)};
+  for (int qg = 0; qg < 2; ++qg) {
+    const int q = q_lo + 16 * qg + (lane & 15);
+    bf16* dp_out = dqkv + ((size_t)b * T + q) * ld + h * D;
+#pragma unroll
+    for (int fd = 0; fd < 4; ++fd)
+      *reinterpret_cast<bf16x4*>(dp_out + 16 * fd + 4 * g) =
+          bf16x4{f2bf(dq[qg][fd][0] * scale), f2bf(dq[qg][fd][1] * scale), f2bf(dq[qg][fd][2] * scale),
+                 f2bf(dq[qg][fd][3] * scale)};
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
-// dK, dV: key-outer over query tiles >= the key block (causal).
-__global__ __launch_bounds__(kThreads) void attn_bwd_dkdv_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
-                                                                 const float* __restrict__ lse, const float* __restrict__ delta,
-                                                                 bf16* __restrict__ dqkv, int T, int H, float scale,
-                                                                 uint64_t seed, uint32_t thr, float inv_keep) {
-  constexpr int kTile = BQ * 128;
-  __shared__ __attribute__((aligned(16))) char smem[2 * (2 * kTile + 2 * BQ * 4)];  // 2 x (Q, dO, lse, delta)
-  constexpr int kStage = 2 * kTile + 2 * BQ * 4;
+// dK, dV: key-outer (128 keys per workgroup, 32 per wave) over 64-query tiles at or after the keys.
+__global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(const bf16* __restrict__ qkv,
+                                                                    const bf16* __restrict__ dout,
+                                                                    const float* __restrict__ lse,
+                                                                    const float* __restrict__ delta,
+                                                                    bf16* __restrict__ dqkv, int T, int H, float scale,
+                                                                    uint64_t seed, uint32_t thr, float inv_keep) {
+  constexpr int kTile = BQT * 128;
+  constexpr int kStage = 2 * kTile + 2 * BQT * 4;
+  __shared__ __attribute__((aligned(16))) char smem[2 * kStage];  // 2 x (Q, dO, lse, delta)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
-  const int nkb = T / BKV;
-  const int kb = blockIdx.x;  // key block; light-to-heavy order does not matter much here
+  const int nqt = T / BQT;
+  const int kb = blockIdx.x;  // key block (heaviest first)
   const int bh = blockIdx.y, b = bh / H, h = bh % H;
   const int C = H * D;
   const size_t ld = 3 * (size_t)C;
   const bf16* base = qkv + (size_t)b * T * ld;
-  const int key = kb * BKV + 16 * w + (lane & 15);
-  bf16x8 kf[2], vf[2];
+  const int k_lo = kb * BKB + 32 * w;  // first key of this wave
+  bf16x8 kf[2][2], vf[2][2];
 #pragma unroll
-  for (int kk = 0; kk < 2; ++kk) {
-    kf[kk] = *reinterpret_cast<const bf16x8*>(base + (size_t)key * ld + C + h * D + 32 * kk + 8 * g);
-    vf[kk] = *reinterpret_cast<const bf16x8*>(base + (size_t)key * ld + 2 * C + h * D + 32 * kk + 8 * g);
-  }
+  for (int kg = 0; kg < 2; ++kg)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const size_t row = (size_t)(k_lo + 16 * kg + (lane & 15)) * ld;
+      kf[kg][kk] = *reinterpret_cast<const bf16x8*>(base + row + C + h * D + 32 * kk + 8 * g);
+      vf[kg][kk] = *reinterpret_cast<const bf16x8*>(base + row + 2 * C + h * D + 32 * kk + 8 * g);
+    }
   const float sl2 = scale * kLog2e;
-  f32x4 dk[4], dv[4];
+  f32x4 dk[2][4], dv[2][4];
 #pragma unroll
-  for (int f = 0; f < 4; ++f) {
-    dk[f] = f32x4{0.f, 0.f, 0.f, 0.f};
-    dv[f] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
+  for (int kg = 0; kg < 2; ++kg)
+#pragma unroll
+    for (int f = 0; f < 4; ++f) dk[kg][f] = dv[kg][f] = f32x4{0.f, 0.f, 0.f, 0.f};
   const bf16* qbase = base + h * D;
   const bf16* dbase = dout + (size_t)b * T * C + h * D;
   const float* lrow = lse + (size_t)bh * T;
@@ -328,83 +390,104 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dkdv_kernel(const bf16* __r
   u32x4 rq[2], rd[2];
   float rl = 0.f, rdl = 0.f;
   auto gload = [&](int i) {
-    tile_load(rq, qbase + (size_t)i * BQ * ld, ld);
-    tile_load(rd, dbase + (size_t)i * BQ * C, C);
-    if (threadIdx.x < BQ) {
-      rl = lrow[i * BQ + threadIdx.x] * kLog2e;
-      rdl = drow[i * BQ + threadIdx.x];
+    tile_load(rq, qbase + (size_t)i * BQT * ld, ld);
+    tile_load(rd, dbase + (size_t)i * BQT * C, C);
+    if (threadIdx.x < BQT) {
+      rl = lrow[i * BQT + threadIdx.x] * kLog2e;
+      rdl = drow[i * BQT + threadIdx.x];
     }
   };
   auto sstore = [&](char* st) {
     tile_store(st, rq);
     tile_store(st + kTile, rd);
-    if (threadIdx.x < BQ) {
+    if (threadIdx.x < BQT) {
       reinterpret_cast<float*>(st + 2 * kTile)[threadIdx.x] = rl;
-      reinterpret_cast<float*>(st + 2 * kTile + BQ * 4)[threadIdx.x] = rdl;
+      reinterpret_cast<float*>(st + 2 * kTile + BQT * 4)[threadIdx.x] = rdl;
     }
   };
-  gload(kb);
+  const int i0 = kb * BKB / BQT;
+  gload(i0);
   sstore(smem);
   __syncthreads();
-  for (int i = kb; i < nkb; ++i) {
-    const int cur = (i - kb) & 1;
+  for (int i = i0; i < nqt; ++i) {
+    const int cur = (i - i0) & 1;
     const char* Qs = smem + cur * kStage;
     const char* Ds = Qs + kTile;
     const float* Ls = reinterpret_cast<const float*>(Qs + 2 * kTile);
-    const float* Dl = Ls + BQ;
-    if (i + 1 < nkb) gload(i + 1);
-    f32x4 s[4], dp[4];
+    const float* Dl = Ls + BQT;
+    if (i + 1 < nqt) gload(i + 1);
+    const int q0 = i * BQT;
+    if (q0 + BQT - 1 >= k_lo) {  // wave-uniform: some query of the tile sees some key of the wave
+      const bool diag = q0 < k_lo + 31;
+      f32x4 s[2][4], dp[2][4];
 #pragma unroll
-    for (int fi = 0; fi < 4; ++fi) {
-      s[fi] = f32x4{0.f, 0.f, 0.f, 0.f};
-      dp[fi] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int fi = 0; fi < 4; ++fi) {
+        s[0][fi] = s[1][fi] = dp[0][fi] = dp[1][fi] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          const bf16x8 qa = row_frag(Qs, 16 * fi, kk, lane);
+          const bf16x8 da = row_frag(Ds, 16 * fi, kk, lane);
+#pragma unroll
+          for (int kg = 0; kg < 2; ++kg) {
+            s[kg][fi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[kg][kk], s[kg][fi], 0, 0, 0);
+            dp[kg][fi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, vf[kg][kk], dp[kg][fi], 0, 0, 0);
+          }
+        }
+      }
+      // s[kg][fi][r] = S[q = q0 + 16fi + 4g + r][key = k_lo + 16kg + (l&15)]
+#pragma unroll
+      for (int fi = 0; fi < 4; ++fi) {
+        const f32x4 l4 = *reinterpret_cast<const f32x4*>(Ls + 16 * fi + 4 * g);
+        const f32x4 d4 = *reinterpret_cast<const f32x4*>(Dl + 16 * fi + 4 * g);
+#pragma unroll
+        for (int kg = 0; kg < 2; ++kg) {
+          const int key = k_lo + 16 * kg + (lane & 15);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int qq = q0 + 16 * fi + 4 * g + r;
+            const float p = (diag && qq < key) ? 0.f : exp2f(s[kg][fi][r] * sl2 - l4[r]);
+            float pdv = p, d = dp[kg][fi][r];
+            if (thr) {
+              const bool keep = drop_keep(seed, att_idx(bh, T, qq, key), thr);
+              pdv = keep ? p * inv_keep : 0.f;
+              d = keep ? d * inv_keep : 0.f;
+            }
+            dp[kg][fi][r] = pdv;               // dropped P (for dV)
+            s[kg][fi][r] = p * (d - d4[r]);    // dS
+          }
+        }
+      }
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
-        s[fi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag(Qs, 16 * fi, kk, lane), kf[kk], s[fi], 0, 0, 0);
-        dp[fi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag(Ds, 16 * fi, kk, lane), vf[kk], dp[fi], 0, 0, 0);
-      }
-    }
-    // s[fi][r] = S[q = 16fi + 4g + r][key]
-    f32x4 pd[4];
+        const bf16x8 p0 = pack_perm(dp[0], kk), p1 = pack_perm(dp[1], kk);
+        const bf16x8 s0 = pack_perm(s[0], kk), s1 = pack_perm(s[1], kk);
 #pragma unroll
-    for (int fi = 0; fi < 4; ++fi) {
-      const f32x4 l4 = *reinterpret_cast<const f32x4*>(Ls + 16 * fi + 4 * g);
-      const f32x4 d4 = *reinterpret_cast<const f32x4*>(Dl + 16 * fi + 4 * g);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int qq = i * BQ + 16 * fi + 4 * g + r;
-        const float p = (qq < key) ? 0.f : exp2f(s[fi][r] * sl2 - l4[r]);
-        float pdv = p, d = dp[fi][r];
-        if (thr) {
-          const bool keep = drop_keep(seed, att_idx(bh, T, qq, key), thr);
-          pdv = keep ? p * inv_keep : 0.f;
-          d = keep ? d * inv_keep : 0.f;
+        for (int fd = 0; fd < 4; ++fd) {
+          const bf16x8 dot = tr_frag(Ds, kk, 16 * fd, lane);
+          const bf16x8 qt = tr_frag(Qs, kk, 16 * fd, lane);
+          dv[0][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dot, p0, dv[0][fd], 0, 0, 0);
+          dv[1][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dot, p1, dv[1][fd], 0, 0, 0);
+          dk[0][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qt, s0, dk[0][fd], 0, 0, 0);
+          dk[1][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qt, s1, dk[1][fd], 0, 0, 0);
         }
-        pd[fi][r] = pdv;
-        s[fi][r] = p * (d - d4[r]);  // dS
       }
     }
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const bf16x8 pf = pack_perm(pd, kk);
-      const bf16x8 sf = pack_perm(s, kk);
-#pragma unroll
-      for (int fd = 0; fd < 4; ++fd) {
-        dv[fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag(Ds, kk, 16 * fd, lane), pf, dv[fd], 0, 0, 0);
-        dk[fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag(Qs, kk, 16 * fd, lane), sf, dk[fd], 0, 0, 0);
-      }
-    }
-    if (i + 1 < nkb) sstore(smem + (cur ^ 1) * kStage);
+    if (i + 1 < nqt) sstore(smem + (cur ^ 1) * kStage);
     __syncthreads();
   }
-  bf16* kout = dqkv + ((size_t)b * T + key) * ld + C + h * D;
-  bf16* vout = kout + C;
 #pragma unroll
-  for (int fd = 0; fd < 4; ++fd) {
-    *reinterpret_cast<bf16x4*>(kout + 16 * fd + 4 * g) = bf16x4{
-        f2bf(dk[fd][0] * scale), f2bf(dk[fd][1] * scale), f2bf(dk[fd][2] * scale), f2bf(dk[fd][3] * scale)};
-    *reinterpret_cast<bf16x4*>(vout + 16 * fd + 4 * g) =
-        bf16x4{f2bf(dv[fd][0]), f2bf(dv[fd][1]), f2bf(dv[fd][2]), f2bf(dv[fd][3])};
+  for (int kg = 0; kg < 2; ++kg) {
+    const int key = k_lo + 16 * kg + (lane & 15);
+    bf16* kout = dqkv + ((size_t)b * T + key) * ld + C + h * D;
+    bf16* vout = kout + C;
+#pragma unroll
+    for (int fd = 0; fd < 4; ++fd) {
+      *reinterpret_cast<bf16x4*>(kout + 16 * fd + 4 * g) =
+          bf16x4{f2bf(dk[kg][fd][0] * scale), f2bf(dk[kg][fd][1] * scale), f2bf(dk[kg][fd][2] * scale),
+                 f2bf(dk[kg][fd][3] * scale)};
+      *reinterpret_cast<bf16x4*>(vout + 16 * fd + 4 * g) =
+          bf16x4{f2bf(dv[kg][fd][0]), f2bf(dv[kg][fd][1]), f2bf(dv[kg][fd][2]), f2bf(dv[kg][fd][3])};
+    }
   }
 }
 
@@ -434,12 +517,11 @@ GPT2MI_EXPORT int gpt2mi_attn_bwd(const uint16_t* qkv, const uint16_t* out, cons
   attn_delta_kernel<<<(B * T * H + 255) / 256, 256, 0, s>>>((const bf16*)out, (const bf16*)dout, delta, B, T, H);
   int rc = gpt2mi::check_launch("attn_delta");
   if (rc) return rc;
-  dim3 grid(T / BQ, B * H);
-  attn_bwd_dkdv_kernel<<<grid, kThreads, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta, (bf16*)dqkv, T, H,
-                                                 scale, seed, thr, ik);
+  attn_bwd_dkdv_kernel<<<dim3(T / BKB, B * H), kThreads, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta,
+                                                                 (bf16*)dqkv, T, H, scale, seed, thr, ik);
   rc = gpt2mi::check_launch("attn_bwd_dkdv");
   if (rc) return rc;
-  attn_bwd_dq_kernel<<<grid, kThreads, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta, (bf16*)dqkv, T, H,
-                                               scale, seed, thr, ik);
+  attn_bwd_dq_kernel<<<dim3(T / BQ, B * H), kThreads, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta,
+                                                              (bf16*)dqkv, T, H, scale, seed, thr, ik);
   return gpt2mi::check_launch("attn_bwd_dq");
 }

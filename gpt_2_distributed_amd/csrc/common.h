@@ -48,14 +48,18 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 
 // ---- counter-based dropout RNG -------------------------------------------------------------------
-// keep(i) is a pure function of (seed, site offset, element index), so backward regenerates the
-// forward mask without storing it. 64-bit splitmix finaliser; 24 random bits compared to p*2^24.
+// keep(i) is a pure function of (seed, element index), so backward regenerates the forward mask
+// without storing it. 32-bit multiply-xorshift finaliser (the element index of every dropout site
+// fits in 32 bits: attention B*H*T*T < 2^32 for every BASELINE config); 24 random bits compared to
+// p*2^24. ~8 VALU ops per element (a 64-bit mixer cost 3-4x that inside the attention loop).
 __device__ __forceinline__ uint32_t drop_bits(uint64_t seed, uint64_t idx) {
-  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (idx + 1);
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z ^= z >> 31;
-  return (uint32_t)(z >> 40);
+  uint32_t h = (uint32_t)idx * 0x9E3779B1u + ((uint32_t)seed ^ (uint32_t)(seed >> 32));
+  h ^= h >> 15;
+  h *= 0x2C1B3C6Du;
+  h ^= h >> 12;
+  h *= 0x297A2D39u;
+  h ^= h >> 15;
+  return h >> 8;
 }
 // threshold = (uint32)(p * 2^24); keep if bits >= threshold.
 __device__ __forceinline__ bool drop_keep(uint64_t seed, uint64_t idx, uint32_t thr) {

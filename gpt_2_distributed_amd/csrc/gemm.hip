@@ -94,13 +94,13 @@ __device__ __forceinline__ float gelu_grad_f(float u) {
 template <bool TRANS, int ROWS>
 struct Loader {
   // TRANS=0: tile is [ROWS][BK] from src[row*ld + k]; TRANS=1: tile is [BK][ROWS] from src[k*ld + row]
-  __device__ __forceinline__ static void load(u32x4* r, const bf16* src, int ld, int row0, int k0) {
+  __device__ __forceinline__ static void load(u32x4* r, const bf16* src, int ld, int row0, int k0, int rmax) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int id = threadIdx.x + kThreads * i;
       const bf16* p;
       if constexpr (!TRANS) {
-        p = src + (size_t)(row0 + id / 8) * ld + k0 + 8 * (id % 8);
+        p = src + (size_t)min(row0 + id / 8, rmax) * ld + k0 + 8 * (id % 8);
       } else {
         p = src + (size_t)(k0 + id / (ROWS / 8)) * ld + row0 + 8 * (id % (ROWS / 8));
       }
@@ -130,7 +130,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams P) {
   const int wm = wid >> 1, wn = wid & 1;
 
   // tile scheduling: XCD-contiguous ranges, grouped-M ordering for L2 reuse
-  const int tiles_m = P.M / BM, tiles_n = P.N / BN;
+  const int tiles_m = (P.M + BM - 1) / BM, tiles_n = P.N / BN;
   const int ntiles = tiles_m * tiles_n;
   const int pid = xcd_remap(blockIdx.x, ntiles);
   constexpr int GM = 8;
@@ -152,8 +152,8 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams P) {
   u32x4 ra[4], rb[4];
   using LA = Loader<A_T, BM>;
   using LB = Loader<B_T, BN>;
-  LA::load(ra, P.A, P.lda, m0, kbeg);
-  LB::load(rb, P.B, P.ldb, n0, kbeg);
+  LA::load(ra, P.A, P.lda, m0, kbeg, P.M - 1);
+  LB::load(rb, P.B, P.ldb, n0, kbeg, P.N - 1);
   LA::store(smem, ra);
   LB::store(smem + BM * BK * 2, rb);
   __syncthreads();
@@ -163,8 +163,8 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams P) {
     const char* As = smem + cur * kStageBytes;
     const char* Bs = As + BM * BK * 2;
     if (kt + 1 < nk) {
-      LA::load(ra, P.A, P.lda, m0, kbeg + (kt + 1) * BK);
-      LB::load(rb, P.B, P.ldb, n0, kbeg + (kt + 1) * BK);
+      LA::load(ra, P.A, P.lda, m0, kbeg + (kt + 1) * BK, P.M - 1);
+      LB::load(rb, P.B, P.ldb, n0, kbeg + (kt + 1) * BK, P.N - 1);
     }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -212,6 +212,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams P) {
     for (int it = 0; it < (BM * BN) / kThreads; ++it) {
       const int id = threadIdx.x + kThreads * it;
       const int row = id / BN, col = id % BN;
+      if (m0 + row >= P.M) continue;
       atomicAdd(C + (size_t)(m0 + row) * P.ldc + n0 + col, alpha * ep[row * kEpiLd + col]);
     }
     return;
@@ -221,6 +222,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams P) {
       const int id = threadIdx.x + kThreads * it;
       const int row = id / (BN / 4), c4 = 4 * (id % (BN / 4));
       const int gm = m0 + row, gn = n0 + c4;
+      if (gm >= P.M) continue;
       f32x4 v = *reinterpret_cast<const f32x4*>(ep + row * kEpiLd + c4);
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[j] *= alpha;
@@ -282,7 +284,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams P) {
 
 template <bool A_T, bool B_T, int EPI>
 int launch(const GemmParams& P, int splits, hipStream_t s) {
-  dim3 grid((P.M / BM) * (P.N / BN), 1, splits);
+  dim3 grid(((P.M + BM - 1) / BM) * (P.N / BN), 1, splits);
   gemm_kernel<A_T, B_T, EPI><<<grid, kThreads, 0, s>>>(P);
   return gpt2mi::check_launch("gemm");
 }
@@ -294,7 +296,8 @@ GPT2MI_EXPORT int gpt2mi_gemm(int layout, int epilogue, int M, int N, int K, con
                               const uint16_t* B, int ldb, void* C, int ldc, const float* bias, const float* resid,
                               uint16_t* aux, int ldaux, float alpha, const float* alpha_dev, int accumulate,
                               int splits, float p_drop, uint64_t seed, void* stream) {
-  GPT2MI_REQUIRE(M % BM == 0 && N % BN == 0, "gemm: M=%d N=%d must be multiples of %d", M, N, BM);
+  GPT2MI_REQUIRE(N % BN == 0 && M % 64 == 0 && M > 0, "gemm: N=%d must be a multiple of %d and M=%d of 64", N, BN, M);
+  GPT2MI_REQUIRE(layout != 2 || M % BM == 0, "gemm: wgrad needs M=%d a multiple of %d", M, BM);
   GPT2MI_REQUIRE(splits >= 1 && K % (BK * splits) == 0, "gemm: K=%d must be a multiple of %d*splits(%d)", K, BK,
                  splits);
   GPT2MI_REQUIRE(splits == 1 || epilogue == EPI_ATOMIC, "gemm: split-K needs the atomic epilogue");

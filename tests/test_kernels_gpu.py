@@ -194,9 +194,20 @@ def test_gemm_gelu_bwd_dgrad():
 
 def test_gemm_rejects_bad_shapes():
     from gpt_2_distributed_amd._lib import KernelError
-    A = torch.zeros(100, 64, dtype=torch.bfloat16, device=dev)
-    with pytest.raises(KernelError, match="multiples of 128"):
-        L().gemm(0, 0, 100, 128, 64, A, 64, A, 64, A, 128)
+    A = torch.zeros(128, 128, dtype=torch.bfloat16, device=dev)
+    with pytest.raises(KernelError, match="multiple of 128"):
+        L().gemm(0, 0, 128, 100, 64, A, 128, A, 128, A, 128)
+    with pytest.raises(KernelError, match="of 64"):
+        L().gemm(0, 0, 100, 128, 64, A, 128, A, 128, A, 128)
+
+
+def test_gemm_partial_m_tile():
+    M, N, K = 192, 256, 128
+    A, W = bf(torch.randn(M, K)), bf(torch.randn(N, K))
+    C = torch.full((M + 64, N), 7.0, device=dev)
+    L().gemm(0, L().EPI_F32, M, N, K, A.to(dev), K, W.to(dev), K, C, N)
+    assert rel_err(C[:M].cpu(), A.float() @ W.float().t()) < 1e-5
+    assert torch.all(C[M:] == 7.0)
 
 
 def _attn_inputs(B, T, H, seed):

@@ -92,8 +92,8 @@ def test_torch_optimizer_and_clip_grad_norm_interop():
         ob.step()
         ob.zero_grad()
         assert abs(na.item() - ob.grad_norm.item()) < 1e-4 * na.item()
-        assert abs(la.item() - lb.item()) < 1e-5 * la.item()
-    assert rel_err(a.arena.cpu(), b.arena.cpu()) < 1e-6
+        assert abs(la.item() - lb.item()) < 1e-4 * la.item()
+    assert rel_err(a.arena.cpu(), b.arena.cpu()) < 1e-5
 
 
 def test_grad_accumulation_equals_big_batch():
