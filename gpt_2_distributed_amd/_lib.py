@@ -38,8 +38,9 @@ _SIGS = {
     "gpt2mi_cast_f32_bf16": [_p, _p, _c_size, _p],
     "gpt2mi_scale_mul": [_p, _p, _p, _p],
     "gpt2mi_memset_zero": [_p, _c_size, _p],
+    "gpt2mi_set_gemm_impl": [_c_int],
 }
-_RESTYPES = {"gpt2mi_last_error": ctypes.c_char_p}
+_RESTYPES = {"gpt2mi_last_error": ctypes.c_char_p, "gpt2mi_set_gemm_impl": None}
 
 EXPORTED = tuple(_SIGS)
 
@@ -158,3 +159,8 @@ def scale_mul(a, b, out):
 
 def zero_(t: torch.Tensor):
     _call("gpt2mi_memset_zero", _ptr(t), t.numel() * t.element_size(), _stream())
+
+
+def set_gemm_impl(impl: int):
+    """0 = auto (256x256 kernel where it applies), 1 = force the 128x128 kernel (A/B benchmarking)."""
+    load().gpt2mi_set_gemm_impl(impl)

@@ -6,7 +6,7 @@ run over a single contiguous fp32 range (one kernel / one bucketed stream of RCC
 
 Layout: parameters in ``GPT2.parameters()`` order (model.py:235-247 module order), each starting
 at a multiple of 64 elements (256 B). ``wte`` is allocated as [Vpad, C] with Vpad = V rounded up to
-128 so the tied lm_head GEMM tiles evenly; rows >= V stay zero forever (zero grad, zero moments).
+256 so the tied lm_head GEMM tiles evenly; rows >= V stay zero forever (zero grad, zero moments).
 """
 from __future__ import annotations
 

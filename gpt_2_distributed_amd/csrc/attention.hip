@@ -90,21 +90,22 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const bf16* __res
                                                                uint64_t seed, uint32_t thr, float inv_keep) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * BKV * 128];  // 2 stages x (K, V)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
-  const int nqb = T / BQ;
+  const int nqb = (T + BQ - 1) / BQ;
   const int qb = nqb - 1 - blockIdx.x;  // heavy (late) query blocks first
   const int bh = blockIdx.y, b = bh / H, h = bh % H;
   const int C = H * D;
   const size_t ld = 3 * (size_t)C;
   const bf16* base = qkv + (size_t)b * T * ld;
   const int q_lo = qb * BQ + 32 * w;  // first query of this wave
+  const bool wave_valid = q_lo < T;    // T % 64 == 0: a wave's 32 queries are all valid or all not
 
   bf16x8 qf[2][2];
 #pragma unroll
   for (int qg = 0; qg < 2; ++qg)
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
-      qf[qg][kk] = *reinterpret_cast<const bf16x8*>(base + (size_t)(q_lo + 16 * qg + (lane & 15)) * ld + h * D +
-                                                    32 * kk + 8 * g);
+      qf[qg][kk] = *reinterpret_cast<const bf16x8*>(
+          base + (size_t)min(q_lo + 16 * qg + (lane & 15), T - 1) * ld + h * D + 32 * kk + 8 * g);
   const float sl2 = scale * kLog2e;
   float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
   f32x4 o[2][4];
@@ -116,7 +117,7 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const bf16* __res
   u32x4 rk[2], rv[2];
   const bf16* kbase = base + C + h * D;
   const bf16* vbase = base + 2 * C + h * D;
-  const int nkv = (qb + 1) * BQ / BKV;
+  const int nkv = min((qb + 1) * BQ, T) / BKV;
   tile_load(rk, kbase, ld);
   tile_load(rv, vbase, ld);
   tile_store(smem, rk);
@@ -132,7 +133,7 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const bf16* __res
       tile_load(rv, vbase + (size_t)(j + 1) * BKV * ld, ld);
     }
     const int k_lo = j * BKV;
-    if (k_lo <= q_lo + 31) {  // wave-uniform: some key of the tile is visible to some query of the wave
+    if (wave_valid && k_lo <= q_lo + 31) {  // wave-uniform: a key of the tile is visible to a query of the wave
       const bool diag = k_lo + BKV - 1 > q_lo;
       f32x4 s[2][4];
 #pragma unroll
@@ -200,6 +201,7 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const bf16* __res
     }
     __syncthreads();
   }
+  if (!wave_valid) return;
 #pragma unroll
   for (int qg = 0; qg < 2; ++qg) {
     const int q = q_lo + 16 * qg + (lane & 15);
@@ -242,18 +244,19 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const bf16* __
                                                                   uint64_t seed, uint32_t thr, float inv_keep) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * BKV * 128];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
-  const int nqb = T / BQ;
+  const int nqb = (T + BQ - 1) / BQ;
   const int qb = nqb - 1 - blockIdx.x;
   const int bh = blockIdx.y, b = bh / H, h = bh % H;
   const int C = H * D;
   const size_t ld = 3 * (size_t)C;
   const bf16* base = qkv + (size_t)b * T * ld;
   const int q_lo = qb * BQ + 32 * w;
+  const bool wave_valid = q_lo < T;
   bf16x8 qf[2][2], df[2][2];
   float lse2[2], dl[2];
 #pragma unroll
   for (int qg = 0; qg < 2; ++qg) {
-    const int q = q_lo + 16 * qg + (lane & 15);
+    const int q = min(q_lo + 16 * qg + (lane & 15), T - 1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       qf[qg][kk] = *reinterpret_cast<const bf16x8*>(base + (size_t)q * ld + h * D + 32 * kk + 8 * g);
@@ -272,7 +275,7 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const bf16* __
   u32x4 rk[2], rv[2];
   const bf16* kbase = base + C + h * D;
   const bf16* vbase = base + 2 * C + h * D;
-  const int nkv = (qb + 1) * BQ / BKV;
+  const int nkv = min((qb + 1) * BQ, T) / BKV;
   tile_load(rk, kbase, ld);
   tile_load(rv, vbase, ld);
   tile_store(smem, rk);
@@ -287,7 +290,7 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const bf16* __
       tile_load(rv, vbase + (size_t)(j + 1) * BKV * ld, ld);
     }
     const int k_lo = j * BKV;
-    if (k_lo <= q_lo + 31) {
+    if (wave_valid && k_lo <= q_lo + 31) {
       const bool diag = k_lo + BKV - 1 > q_lo;
       f32x4 s[2][4], dp[2][4];
 #pragma unroll
@@ -336,6 +339,7 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const bf16* __
     }
     __syncthreads();
   }
+  if (!wave_valid) return;
 #pragma unroll
   for (int qg = 0; qg < 2; ++qg) {
     const int q = q_lo + 16 * qg + (lane & 15);
@@ -367,12 +371,13 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(const bf16* 
   const size_t ld = 3 * (size_t)C;
   const bf16* base = qkv + (size_t)b * T * ld;
   const int k_lo = kb * BKB + 32 * w;  // first key of this wave
+  const bool wave_valid = k_lo < T;
   bf16x8 kf[2][2], vf[2][2];
 #pragma unroll
   for (int kg = 0; kg < 2; ++kg)
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      const size_t row = (size_t)(k_lo + 16 * kg + (lane & 15)) * ld;
+      const size_t row = (size_t)min(k_lo + 16 * kg + (lane & 15), T - 1) * ld;
       kf[kg][kk] = *reinterpret_cast<const bf16x8*>(base + row + C + h * D + 32 * kk + 8 * g);
       vf[kg][kk] = *reinterpret_cast<const bf16x8*>(base + row + 2 * C + h * D + 32 * kk + 8 * g);
     }
@@ -417,7 +422,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(const bf16* 
     const float* Dl = Ls + BQT;
     if (i + 1 < nqt) gload(i + 1);
     const int q0 = i * BQT;
-    if (q0 + BQT - 1 >= k_lo) {  // wave-uniform: some query of the tile sees some key of the wave
+    if (wave_valid && q0 + BQT - 1 >= k_lo) {  // wave-uniform: a query of the tile sees a key of the wave
       const bool diag = q0 < k_lo + 31;
       f32x4 s[2][4], dp[2][4];
 #pragma unroll
@@ -475,6 +480,7 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(const bf16* 
     if (i + 1 < nqt) sstore(smem + (cur ^ 1) * kStage);
     __syncthreads();
   }
+  if (!wave_valid) return;
 #pragma unroll
   for (int kg = 0; kg < 2; ++kg) {
     const int key = k_lo + 16 * kg + (lane & 15);
@@ -496,9 +502,9 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(const bf16* 
 GPT2MI_EXPORT int gpt2mi_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int T, int H, int head_dim,
                                   float p_drop, uint64_t seed, void* stream) {
   GPT2MI_REQUIRE(head_dim == D, "attn_fwd: head_dim=%d (only 64 is built)", head_dim);
-  GPT2MI_REQUIRE(T % BQ == 0 && T > 0, "attn_fwd: T=%d must be a multiple of %d", T, BQ);
+  GPT2MI_REQUIRE(T % 64 == 0 && T > 0, "attn_fwd: T=%d must be a multiple of 64", T);
   const float scale = 1.f / sqrtf((float)head_dim);
-  dim3 grid(T / BQ, B * H);
+  dim3 grid((T + BQ - 1) / BQ, B * H);
   attn_fwd_kernel<<<grid, kThreads, 0, (hipStream_t)stream>>>((const bf16*)qkv, (bf16*)out, lse, T, H, scale, seed,
                                                               drop_threshold(p_drop),
                                                               p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f);
@@ -509,7 +515,7 @@ GPT2MI_EXPORT int gpt2mi_attn_bwd(const uint16_t* qkv, const uint16_t* out, cons
                                   float* delta, uint16_t* dqkv, int B, int T, int H, int head_dim, float p_drop,
                                   uint64_t seed, void* stream) {
   GPT2MI_REQUIRE(head_dim == D, "attn_bwd: head_dim=%d (only 64 is built)", head_dim);
-  GPT2MI_REQUIRE(T % BQ == 0 && T > 0, "attn_bwd: T=%d must be a multiple of %d", T, BQ);
+  GPT2MI_REQUIRE(T % 64 == 0 && T > 0, "attn_bwd: T=%d must be a multiple of 64", T);
   hipStream_t s = (hipStream_t)stream;
   const float scale = 1.f / sqrtf((float)head_dim);
   const uint32_t thr = drop_threshold(p_drop);
@@ -517,11 +523,11 @@ GPT2MI_EXPORT int gpt2mi_attn_bwd(const uint16_t* qkv, const uint16_t* out, cons
   attn_delta_kernel<<<(B * T * H + 255) / 256, 256, 0, s>>>((const bf16*)out, (const bf16*)dout, delta, B, T, H);
   int rc = gpt2mi::check_launch("attn_delta");
   if (rc) return rc;
-  attn_bwd_dkdv_kernel<<<dim3(T / BKB, B * H), kThreads, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta,
+  attn_bwd_dkdv_kernel<<<dim3((T + BKB - 1) / BKB, B * H), kThreads, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta,
                                                                  (bf16*)dqkv, T, H, scale, seed, thr, ik);
   rc = gpt2mi::check_launch("attn_bwd_dkdv");
   if (rc) return rc;
-  attn_bwd_dq_kernel<<<dim3(T / BQ, B * H), kThreads, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta,
+  attn_bwd_dq_kernel<<<dim3((T + BQ - 1) / BQ, B * H), kThreads, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta,
                                                               (bf16*)dqkv, T, H, scale, seed, thr, ik);
   return gpt2mi::check_launch("attn_bwd_dq");
 }

@@ -18,40 +18,15 @@
 //                          -> fragments by two conflict-free ds_read_b64_tr_b16 (hardware transpose).
 // Epilogue: accumulators -> LDS (fp32, padded rows) -> row-contiguous 16-B chunks -> fused op -> HBM.
 #include "common.h"
+#include "gemm_common.h"
 
 namespace {
-
-enum Epi : int {
-  EPI_BF16 = 0,      // C_bf16 = alpha*acc (+bias)
-  EPI_F32 = 1,       // C_f32 (+)= alpha*acc (+bias)           (beta = accumulate flag)
-  EPI_RESID = 2,     // C_f32 = resid_f32 + drop(alpha*acc + bias)
-  EPI_GELU = 3,      // aux_bf16 = u = acc+bias ; C_bf16 = drop(gelu(u))
-  EPI_GELU_BWD = 4,  // C_bf16 = drop_mask(alpha*acc) * gelu'(aux_bf16)
-  EPI_ATOMIC = 5,    // atomicAdd(C_f32, alpha*acc)            (split-K / accumulation)
-};
 
 constexpr int BM = 128, BN = 128, BK = 64;
 constexpr int kThreads = 256;
 constexpr int kStageBytes = (BM + BN) * BK * 2;           // 32 KiB
 constexpr int kEpiLd = BN + 4;                            // fp32 epilogue row stride (floats)
 constexpr int kLdsBytes = (2 * kStageBytes > BM * kEpiLd * 4) ? 2 * kStageBytes : BM * kEpiLd * 4;
-
-struct GemmParams {
-  const bf16* A;
-  const bf16* B;
-  void* C;
-  const float* bias;
-  const float* resid;
-  bf16* aux;  // EPI_GELU: pre-activation out; EPI_GELU_BWD: pre-activation in
-  const float* alpha_dev;
-  int M, N, K, lda, ldb, ldc, ldaux;
-  int k_per_split;
-  float alpha;
-  int accumulate;
-  uint64_t seed;
-  uint32_t thr;
-  float inv_keep;
-};
 
 __device__ __forceinline__ int kc_off(int row, int chunk) { return row * 128 + 16 * (chunk ^ (row & 7)); }
 __device__ __forceinline__ int mc_swz(int k) { return 2 * ((k & 3) | (((k >> 3) & 1) << 2)); }
@@ -75,19 +50,6 @@ __device__ __forceinline__ bf16x8 read_frag_mc(const char* base, int k0, int m0,
   typedef short s16x8 __attribute__((ext_vector_type(8)));
   s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   return __builtin_bit_cast(bf16x8, r);
-}
-
-__device__ __forceinline__ float gelu_f(float u) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  const float z = k0 * (u + k1 * u * u * u);
-  const float t = 1.f - 2.f / (__expf(2.f * z) + 1.f);  // tanh(z)
-  return 0.5f * u * (1.f + t);
-}
-__device__ __forceinline__ float gelu_grad_f(float u) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  const float z = k0 * (u + k1 * u * u * u);
-  const float t = 1.f - 2.f / (__expf(2.f * z) + 1.f);
-  return 0.5f * (1.f + t) + 0.5f * u * (1.f - t * t) * k0 * (1.f + 3.f * k1 * u * u);
 }
 
 // Tile loader: 4 x 16-B chunks per thread per operand per K-tile.
@@ -231,53 +193,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams P) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] += b[j];
       }
-      const size_t cidx = (size_t)gm * P.ldc + gn;
-      const uint64_t didx = (uint64_t)gm * P.N + gn;  // dropout element index in the logical [M,N]
-      if constexpr (EPI == EPI_BF16) {
-        bf16* C = reinterpret_cast<bf16*>(P.C);
-        *reinterpret_cast<bf16x4*>(C + cidx) = bf16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
-      } else if constexpr (EPI == EPI_F32) {
-        float* C = reinterpret_cast<float*>(P.C);
-        if (P.accumulate) {
-          f32x4 o = *reinterpret_cast<const f32x4*>(C + cidx);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] += o[j];
-        }
-        *reinterpret_cast<f32x4*>(C + cidx) = v;
-      } else if constexpr (EPI == EPI_RESID) {
-        float* C = reinterpret_cast<float*>(P.C);
-        f32x4 r = *reinterpret_cast<const f32x4*>(P.resid + cidx);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          float y = v[j];
-          if (P.thr) y = drop_keep(P.seed, didx + j, P.thr) ? y * P.inv_keep : 0.f;
-          r[j] += y;
-        }
-        *reinterpret_cast<f32x4*>(C + cidx) = r;
-      } else if constexpr (EPI == EPI_GELU) {
-        bf16* C = reinterpret_cast<bf16*>(P.C);
-        bf16x4 u, h;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          u[j] = f2bf(v[j]);
-          float a = gelu_f(v[j]);
-          if (P.thr) a = drop_keep(P.seed, didx + j, P.thr) ? a * P.inv_keep : 0.f;
-          h[j] = f2bf(a);
-        }
-        *reinterpret_cast<bf16x4*>(P.aux + (size_t)gm * P.ldaux + gn) = u;
-        *reinterpret_cast<bf16x4*>(C + cidx) = h;
-      } else if constexpr (EPI == EPI_GELU_BWD) {
-        bf16* C = reinterpret_cast<bf16*>(P.C);
-        bf16x4 u = *reinterpret_cast<const bf16x4*>(P.aux + (size_t)gm * P.ldaux + gn);
-        bf16x4 o;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          float d = v[j];
-          if (P.thr) d = drop_keep(P.seed, didx + j, P.thr) ? d * P.inv_keep : 0.f;
-          o[j] = f2bf(d * gelu_grad_f(bf2f(u[j])));
-        }
-        *reinterpret_cast<bf16x4*>(C + cidx) = o;
-      }
+      epilogue_store<EPI>(P, gm, gn, v);
     }
   }
 }
@@ -290,6 +206,9 @@ int launch(const GemmParams& P, int splits, hipStream_t s) {
 }
 
 }  // namespace
+
+static int g_gemm_impl = 0;  // 0 auto, 1 force the 128x128 kernel (A/B benchmarking)
+GPT2MI_EXPORT void gpt2mi_set_gemm_impl(int impl) { g_gemm_impl = impl; }
 
 // layout: 0 = forward (A[M][K], B[N][K]); 1 = dgrad (A[M][K], B[K][N]); 2 = wgrad (A[K][M], B[K][N]).
 GPT2MI_EXPORT int gpt2mi_gemm(int layout, int epilogue, int M, int N, int K, const uint16_t* A, int lda,
@@ -320,6 +239,11 @@ GPT2MI_EXPORT int gpt2mi_gemm(int layout, int epilogue, int M, int N, int K, con
   P.thr = drop_threshold(p_drop);
   P.inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
   hipStream_t s = (hipStream_t)stream;
+  const bool big_ok = splits == 1 && layout <= 1 && N % 256 == 0 && epilogue != EPI_ATOMIC;
+  if (big_ok && g_gemm_impl != 1) {
+    const int rc = gpt2mi::gemm256_dispatch(layout, epilogue, P, s);
+    if (rc >= 0) return rc;
+  }
   switch (layout * 16 + epilogue) {
     case 0 * 16 + EPI_BF16: return launch<false, false, EPI_BF16>(P, splits, s);
     case 0 * 16 + EPI_F32: return launch<false, false, EPI_F32>(P, splits, s);

@@ -1,0 +1,103 @@
+// Shared GEMM parameter block and fused epilogue ops (gemm.hip: 128x128 kernel; gemm256.hip).
+#pragma once
+#include "common.h"
+
+enum Epi : int {
+  EPI_BF16 = 0,      // C_bf16 = alpha*acc (+bias)
+  EPI_F32 = 1,       // C_f32 (+)= alpha*acc (+bias)           (accumulate flag)
+  EPI_RESID = 2,     // C_f32 = resid_f32 + drop(alpha*acc + bias)          (proj / fc2 + residual)
+  EPI_GELU = 3,      // aux_bf16 = u = acc+bias ; C_bf16 = drop(gelu_tanh(u))   (fc1 + NewGELU + drop1)
+  EPI_GELU_BWD = 4,  // C_bf16 = drop_mask(alpha*acc) * gelu'(aux_bf16)        (fc2 dgrad -> fc1 output grad)
+  EPI_ATOMIC = 5,    // atomicAdd(C_f32, alpha*acc)            (split-K wgrad into the grad arena)
+};
+
+struct GemmParams {
+  const bf16* A;
+  const bf16* B;
+  void* C;
+  const float* bias;
+  const float* resid;
+  bf16* aux;  // EPI_GELU: pre-activation out; EPI_GELU_BWD: pre-activation in
+  const float* alpha_dev;
+  int M, N, K, lda, ldb, ldc, ldaux;
+  int k_per_split;
+  float alpha;
+  int accumulate;
+  uint64_t seed;
+  uint32_t thr;
+  float inv_keep;
+};
+
+// NewGELU (model.py:63-77) with tanh(z) = 1 - 2/(exp(2z)+1)
+__device__ __forceinline__ float gelu_f(float u) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float z = k0 * (u + k1 * u * u * u);
+  const float t = 1.f - 2.f / (__expf(2.f * z) + 1.f);
+  return 0.5f * u * (1.f + t);
+}
+__device__ __forceinline__ float gelu_grad_f(float u) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float z = k0 * (u + k1 * u * u * u);
+  const float t = 1.f - 2.f / (__expf(2.f * z) + 1.f);
+  return 0.5f * (1.f + t) + 0.5f * u * (1.f - t * t) * k0 * (1.f + 3.f * k1 * u * u);
+}
+
+// Apply the fused epilogue to 4 consecutive outputs C[gm][gn..gn+3]; v = alpha*acc (+bias).
+template <int EPI>
+__device__ __forceinline__ void epilogue_store(const GemmParams& P, int gm, int gn, f32x4 v) {
+  const size_t cidx = (size_t)gm * P.ldc + gn;
+  const uint64_t didx = (uint64_t)gm * P.N + gn;  // dropout element index in the logical [M,N]
+  if constexpr (EPI == EPI_BF16) {
+    bf16* C = reinterpret_cast<bf16*>(P.C);
+    *reinterpret_cast<bf16x4*>(C + cidx) = bf16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+  } else if constexpr (EPI == EPI_F32) {
+    float* C = reinterpret_cast<float*>(P.C);
+    if (P.accumulate) {
+      f32x4 o = *reinterpret_cast<const f32x4*>(C + cidx);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] += o[j];
+    }
+    *reinterpret_cast<f32x4*>(C + cidx) = v;
+  } else if constexpr (EPI == EPI_RESID) {
+    float* C = reinterpret_cast<float*>(P.C);
+    f32x4 r = *reinterpret_cast<const f32x4*>(P.resid + cidx);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float y = v[j];
+      if (P.thr) y = drop_keep(P.seed, didx + j, P.thr) ? y * P.inv_keep : 0.f;
+      r[j] += y;
+    }
+    *reinterpret_cast<f32x4*>(C + cidx) = r;
+  } else if constexpr (EPI == EPI_GELU) {
+    bf16* C = reinterpret_cast<bf16*>(P.C);
+    bf16x4 u, h;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      u[j] = f2bf(v[j]);
+      float a = gelu_f(v[j]);
+      if (P.thr) a = drop_keep(P.seed, didx + j, P.thr) ? a * P.inv_keep : 0.f;
+      h[j] = f2bf(a);
+    }
+    *reinterpret_cast<bf16x4*>(P.aux + (size_t)gm * P.ldaux + gn) = u;
+    *reinterpret_cast<bf16x4*>(C + cidx) = h;
+  } else if constexpr (EPI == EPI_GELU_BWD) {
+    bf16* C = reinterpret_cast<bf16*>(P.C);
+    bf16x4 u = *reinterpret_cast<const bf16x4*>(P.aux + (size_t)gm * P.ldaux + gn);
+    bf16x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float d = v[j];
+      if (P.thr) d = drop_keep(P.seed, didx + j, P.thr) ? d * P.inv_keep : 0.f;
+      o[j] = f2bf(d * gelu_grad_f(bf2f(u[j])));
+    }
+    *reinterpret_cast<bf16x4*>(C + cidx) = o;
+  } else if constexpr (EPI == EPI_ATOMIC) {
+    float* C = reinterpret_cast<float*>(P.C);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) atomicAdd(C + cidx + j, v[j]);
+  }
+}
+
+namespace gpt2mi {
+int gemm256_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t s);
+}

@@ -10,7 +10,7 @@ north star names are exported too: ``GPT = GPT2``, ``forward(idx, targets=...)``
 
 What differs underneath (MI355X-first):
 * all parameters live in one flat fp32 arena (``arena.py``) so AdamW / grad-norm / collectives are
-  single passes; ``wte`` is padded to a multiple of 128 rows for the lm_head tiling;
+  single passes; ``wte`` is padded to a multiple of 256 rows for the lm_head tiling;
 * ``GPT2.forward`` is ONE autograd node: forward and backward of the whole network are explicit
   sequences of HIP kernels (``engine.py``) with bf16 MFMA GEMMs, fused epilogues, flash attention;
   it always computes with the CUDA-autocast-bf16 numerics of the reference trainer
@@ -151,7 +151,7 @@ class GPT2(nn.Module):
     # ---- flat arena ------------------------------------------------------------------------------
     def _pack_arena(self):
         cfg = self.config
-        self.vpad = round_up(cfg.vocab_size, 128)
+        self.vpad = round_up(cfg.vocab_size, 256)
         names = [n for n, _ in self.named_parameters()]
         shapes = {n: tuple(p.shape) for n, p in self.named_parameters()}
         from collections import OrderedDict

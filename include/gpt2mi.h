@@ -87,6 +87,10 @@ int gpt2mi_adamw(float* p, const float* g, float* m, float* v, uint16_t* p_bf16,
 int gpt2mi_grad_norm(const float* g, size_t n, float scale, float* partials, float* out, void* stream);
 int gpt2mi_norm_partials_size(void);
 
+/* GEMM kernel selection for A/B benchmarking: 0 = auto (256x256 tiles for layouts 0/1 when N % 256 == 0),
+ * 1 = always the 128x128 kernel. */
+void gpt2mi_set_gemm_impl(int impl);
+
 int gpt2mi_cast_f32_bf16(const float* x, uint16_t* y, size_t n, void* stream);
 int gpt2mi_scale_mul(const float* a, const float* b, float* out, void* stream);
 int gpt2mi_memset_zero(void* ptr, size_t bytes, void* stream);

@@ -335,3 +335,27 @@ def test_colsum():
     db = torch.ones(N, device=dev)
     L().colsum_bf16(g.to(dev), db, M, N, N)
     assert rel_err(db.cpu(), 1 + g.float().sum(0)) < 1e-5
+
+
+@pytest.mark.parametrize("layout,epi", [(0, 0), (0, 2), (0, 3), (1, 0), (1, 4)])
+def test_gemm256_matches_gemm128(layout, epi):
+    """The 256x256 LDS-DMA kernel and the 128x128 kernel agree on every fused epilogue (incl. dropout)."""
+    M, N, K = 320, 768, 192  # partial 256-row tile
+    g = torch.Generator().manual_seed(layout * 10 + epi)
+    A = bf(torch.randn(M, K, generator=g)).to(dev)
+    Bm = bf(torch.randn(N, K, generator=g) if layout == 0 else torch.randn(K, N, generator=g)).to(dev)
+    ldb = K if layout == 0 else N
+    bias = torch.randn(N, generator=g).to(dev)
+    resid = torch.randn(M, N, generator=g).to(dev)
+    outs = []
+    for impl in (0, 1):
+        L().set_gemm_impl(impl)
+        f32 = epi == 2
+        C = torch.zeros(M, N, device=dev, dtype=torch.float32 if f32 else torch.bfloat16)
+        aux = bf(torch.randn(M, N, generator=torch.Generator().manual_seed(5))).to(dev)
+        L().gemm(layout, epi, M, N, K, A, K, Bm, ldb, C, N, bias=bias if layout == 0 else None,
+                 resid=resid if epi == 2 else None, aux=aux, ldaux=N, p_drop=0.1, seed=77)
+        outs.append((C.float().cpu(), aux.float().cpu()))
+    L().set_gemm_impl(0)
+    assert rel_err(outs[0][0], outs[1][0]) < 1e-5 if epi == 2 else rel_err(outs[0][0], outs[1][0]) < 2e-3
+    assert rel_err(outs[0][1], outs[1][1]) < 2e-3

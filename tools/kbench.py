@@ -51,13 +51,13 @@ def gemm(M=65536):
         ("fc1 fwd gelu", 0, K.EPI_GELU, M, 4 * C, C),
         ("fc2 fwd resid", 0, K.EPI_RESID, M, C, 4 * C),
         ("proj fwd resid", 0, K.EPI_RESID, M, C, C),
-        ("lm_head fwd", 0, K.EPI_BF16, M, 50304, C),
+        ("lm_head fwd", 0, K.EPI_BF16, M, 50432, C),
         ("fc2 dgrad gelu", 1, K.EPI_GELU_BWD, M, 4 * C, C),
         ("qkv dgrad", 1, K.EPI_BF16, M, C, 3 * C),
-        ("lm dgrad", 1, K.EPI_BF16, M, C, 50304),
+        ("lm dgrad", 1, K.EPI_BF16, M, C, 50432),
         ("fc1 wgrad", 2, K.EPI_ATOMIC, 4 * C, C, M),
         ("qkv wgrad", 2, K.EPI_ATOMIC, 3 * C, C, M),
-        ("lm wgrad", 2, K.EPI_F32, 50304, C, M),
+        ("lm wgrad", 2, K.EPI_F32, 50432, C, M),
     ]
     for name, lay, epi, m, n, k in shapes:
         if lay == 0:
@@ -98,4 +98,8 @@ if __name__ == "__main__":
         attn(p=0.0)
         attn(p=0.1)
     if "gemm" in what:
-        gemm()
+        for impl in (0, 1):
+            print(f"--- gemm impl {impl} ({'auto: 256x256 for fwd/dgrad' if impl == 0 else '128x128 only'})")
+            K.set_gemm_impl(impl)
+            gemm()
+        K.set_gemm_impl(0)
