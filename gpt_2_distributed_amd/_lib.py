@@ -39,6 +39,8 @@ _SIGS = {
     "gpt2mi_scale_mul": [_p, _p, _p, _p],
     "gpt2mi_memset_zero": [_p, _c_size, _p],
     "gpt2mi_set_gemm_impl": [_c_int],
+    "gpt2mi_gemm_wgrad": [_c_int, _c_int, _c_int, _p, _c_int, _p, _c_int, _p, _c_int, _c_int, _c_float, _p, _p,
+                          _c_size, _c_int, _p],
 }
 _RESTYPES = {"gpt2mi_last_error": ctypes.c_char_p, "gpt2mi_set_gemm_impl": None}
 
@@ -120,6 +122,19 @@ def gemm(layout, epilogue, M, N, K, A, lda, B, ldb, C, ldc, bias=None, resid=Non
          alpha=1.0, alpha_dev=None, accumulate=False, splits=1, p_drop=0.0, seed=0):
     _call("gpt2mi_gemm", layout, epilogue, M, N, K, _ptr(A), lda, _ptr(B), ldb, _ptr(C), ldc, _ptr(bias),
           _ptr(resid), _ptr(aux), ldaux, alpha, _ptr(alpha_dev), int(accumulate), splits, p_drop, seed, _stream())
+
+
+def gemm_wgrad(M, N, K, A, lda, B, ldb, C, ldc, accumulate=True, alpha=1.0, alpha_dev=None, workspace=None,
+               splits=1):
+    ws_n = workspace.numel() if workspace is not None else 0
+    _call("gpt2mi_gemm_wgrad", M, N, K, _ptr(A), lda, _ptr(B), ldb, _ptr(C), ldc, int(accumulate), alpha,
+          _ptr(alpha_dev), _ptr(workspace), ws_n, splits, _stream())
+
+
+def wgrad_splits(M, N, cus=256):
+    """Split-K factor for a wgrad output of M x N on 256x256 tiles: fill one wave of the 256 CUs."""
+    tiles = (M // 256) * (N // 256)
+    return 1 if tiles >= cus else max(1, cus // tiles)
 
 
 def attn_fwd(qkv, out, lse, B, T, H, D, p_drop=0.0, seed=0):

@@ -239,9 +239,9 @@ GPT2MI_EXPORT int gpt2mi_gemm(int layout, int epilogue, int M, int N, int K, con
   P.thr = drop_threshold(p_drop);
   P.inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
   hipStream_t s = (hipStream_t)stream;
-  const bool big_ok = splits == 1 && layout <= 1 && N % 256 == 0 && epilogue != EPI_ATOMIC;
+  const bool big_ok = splits == 1 && N % 256 == 0 && epilogue != EPI_ATOMIC && (layout <= 1 || M % 256 == 0);
   if (big_ok && g_gemm_impl != 1) {
-    const int rc = gpt2mi::gemm256_dispatch(layout, epilogue, P, s);
+    const int rc = gpt2mi::gemm256_dispatch(layout, epilogue, P, s, 1);
     if (rc >= 0) return rc;
   }
   switch (layout * 16 + epilogue) {
@@ -258,4 +258,38 @@ GPT2MI_EXPORT int gpt2mi_gemm(int layout, int epilogue, int M, int N, int K, con
       gpt2mi::set_error("gemm: unsupported layout %d / epilogue %d combination", layout, epilogue);
       return 22;
   }
+}
+
+// Weight gradient C[M][N] (+)= alpha * A^T B with A stored [K][M], B stored [K][N] (dW = dY^T X over
+// K = tokens), on the 256x256 kernel: `splits` K ranges write fp32 partial slabs into `workspace`
+// (splits*M*N floats), then one pass sums them in fixed order into C (deterministic; no atomics).
+GPT2MI_EXPORT int gpt2mi_gemm_wgrad(int M, int N, int K, const uint16_t* A, int lda, const uint16_t* B, int ldb,
+                                    float* C, int ldc, int accumulate, float alpha, const float* alpha_dev,
+                                    float* workspace, size_t workspace_floats, int splits, void* stream) {
+  GPT2MI_REQUIRE(M % 256 == 0 && N % 256 == 0 && K % 64 == 0, "gemm_wgrad: M=%d N=%d must be multiples of 256, K=%d of 64",
+                 M, N, K);
+  GPT2MI_REQUIRE(ldc == N, "gemm_wgrad: C must be dense (ldc == N)");
+  GPT2MI_REQUIRE(splits >= 1 && splits <= K / 64, "gemm_wgrad: bad splits %d", splits);
+  hipStream_t s = (hipStream_t)stream;
+  GemmParams P{};
+  P.A = (const bf16*)A;
+  P.B = (const bf16*)B;
+  P.M = M; P.N = N; P.K = K; P.lda = lda; P.ldb = ldb; P.ldc = ldc;
+  P.alpha = alpha;
+  P.alpha_dev = alpha_dev;
+  P.accumulate = accumulate;
+  const int ktiles = K / 64;
+  P.k_per_split = ((ktiles + splits - 1) / splits) * 64;
+  splits = (K + P.k_per_split - 1) / P.k_per_split;
+  if (splits == 1) {
+    P.C = C;
+    return gpt2mi::gemm256_dispatch(2, EPI_F32, P, s, 1);
+  }
+  GPT2MI_REQUIRE(workspace != nullptr && workspace_floats >= (size_t)splits * M * N,
+                 "gemm_wgrad: workspace of %zu floats < splits*M*N = %zu", workspace_floats, (size_t)splits * M * N);
+  P.C = workspace;
+  P.accumulate = 0;
+  int rc = gpt2mi::gemm256_dispatch(2, EPI_SLAB, P, s, splits);
+  if (rc) return rc;
+  return gpt2mi::splitk_reduce(workspace, splits, (size_t)M * N, C, accumulate, s);
 }

@@ -1,15 +1,18 @@
 // bf16 MFMA GEMM, 256x256 block tile — the forward / dgrad workhorse (see gemm.hip for the API).
 //
 // 512 threads = 8 waves as 2 (M) x 4 (N), 128x64 outputs per wave (8x4 v_mfma_f32_16x16x32_bf16
-// accumulators, 128 registers), BK = 32, one workgroup per CU, 4-stage LDS ring (4 x 32 KiB).
-// Global->LDS by global_load_lds_dwordx4 (LDS-DMA, no register staging), 4 instructions per wave
-// per K-tile. Three K-tiles are in flight while one is consumed: each iteration waits with a
-// COUNTED vmcnt for its own tile only (never vmcnt(0) in the loop), crosses one raw s_barrier
-// (which also frees the stage read in the previous iteration) and refills that stage with tile
-// kt+3 before issuing its 32 MFMAs. The DMA destination is lane-linear, so the bank-conflict XOR
-// swizzle is applied on the SOURCE address and undone on the ds_read:
-//   k-contiguous operand image [256][32] : chunk c of row r at (c ^ ((r>>3 & 1) << 1))  (ds_read_b128)
-//   m-contiguous operand image [32][256] : chunk c of k-row k at (c ^ 2((k&3)|((k>>3&1)<<2)))
+// accumulators, 128 registers), BK = 64, one workgroup per CU, 2 LDS stages (2 x 64 KiB).
+// Global->LDS by global_load_lds_dwordx4 (LDS-DMA, no register staging), 8 instructions per wave
+// per K-tile, issued for tile kt+1 before the MFMAs of tile kt and retired by one vmcnt(0) +
+// barrier per K-tile. Measured alternatives that were slower on MI355X (tools/kbench.py): a 4-stage
+// BK=32 ring with counted vmcnt (twice the barriers per MFMA) and register double-buffering of
+// the fragments (the compiler already overlaps the ds_reads; +70 VGPRs).
+// Split-K (wgrad): blockIdx.y selects a K range; each split writes its fp32 partial tile to a slab
+// and gpt2mi_gemm_wgrad sums the slabs into the gradient in a second, deterministic pass.
+// The DMA destination is lane-linear, so the bank-conflict XOR swizzle is applied on the SOURCE
+// address and undone on the ds_read:
+//   k-contiguous operand image [256][64] : chunk c of row r at (c ^ (r & 7))            (ds_read_b128)
+//   m-contiguous operand image [64][256] : chunk c of k-row k at (c ^ 2((k&3)|((k>>3&1)<<2)))
 //                                          (two ds_read_b64_tr_b16 per fragment)
 // Epilogue straight from registers: the MFMA is issued as D^T = B.A^T, so each lane holds FOUR
 // CONSECUTIVE output columns of one row -> 8-B (bf16) / 16-B (fp32) stores and 16-B bias /
@@ -19,32 +22,30 @@
 
 namespace {
 
-constexpr int BM = 256, BN = 256, BK = 32;
+constexpr int BM = 256, BN = 256, BK = 64;
 constexpr int kThreads = 512;
-constexpr int kStages = 4;
-constexpr int kOpBytes = BM * BK * 2;             // 16 KiB per operand per stage
-constexpr int kStageBytes = 2 * kOpBytes;         // 32 KiB
-constexpr int kLdsBytes = kStages * kStageBytes;  // 128 KiB
+constexpr int kOpBytes = BM * BK * 2;       // 32 KiB per operand per stage
+constexpr int kStageBytes = 2 * kOpBytes;   // 64 KiB
+constexpr int kLdsBytes = 2 * kStageBytes;  // 128 KiB
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
-__device__ __forceinline__ int kc_swz(int row) { return ((row >> 3) & 1) << 1; }
-__device__ __forceinline__ int kc_off(int row, int chunk) { return row * 64 + 16 * (chunk ^ kc_swz(row)); }
+__device__ __forceinline__ int kc_off(int row, int chunk) { return row * 128 + 16 * (chunk ^ (row & 7)); }
 __device__ __forceinline__ int mc_swz(int k) { return 2 * ((k & 3) | (((k >> 3) & 1) << 2)); }
 __device__ __forceinline__ int mc_off(int k, int chunk) { return k * 512 + 16 * (chunk ^ mc_swz(k)); }
 
-// One operand's K-tile by LDS-DMA: 16 x 1 KiB instructions per tile, 2 per wave.
+// One operand's K-tile by LDS-DMA: 32 x 1 KiB instructions per tile, 4 per wave.
 template <bool TRANS>
 __device__ __forceinline__ void dma_tile(const bf16* __restrict__ src, int ld, int row0, int k0, int rmax, char* tile,
                                          int wid, int lane) {
 #pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int ins = wid * 2 + t;
+  for (int t = 0; t < 4; ++t) {
+    const int ins = wid * 4 + t;
     const bf16* g;
-    if constexpr (!TRANS) {  // instruction covers rows 16*ins .. +16 (64 B each)
-      const int row = 16 * ins + (lane >> 2);
-      const int c = (lane & 3) ^ kc_swz(row);
+    if constexpr (!TRANS) {  // instruction covers rows 8*ins .. +8 (128 B each)
+      const int row = 8 * ins + (lane >> 3);
+      const int c = (lane & 7) ^ (row & 7);
       g = src + (size_t)min(row0 + row, rmax) * ld + k0 + 8 * c;
     } else {  // instruction covers k-rows 2*ins, 2*ins+1 (512 B each)
       const int k = 2 * ins + (lane >> 5);
@@ -86,7 +87,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm256_kernel(GemmParams P) {
   const int tm = first_m + (pid % (GM * tiles_n)) % gsz;
   const int tn = (pid % (GM * tiles_n)) / gsz;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int nk = P.K / BK;
+  const int kbeg = blockIdx.y * P.k_per_split;
+  const int nk = (min(P.K, kbeg + P.k_per_split) - kbeg) / BK;
 
   f32x4 acc[8][4];
 #pragma unroll
@@ -94,38 +96,36 @@ __global__ __launch_bounds__(kThreads, 1) void gemm256_kernel(GemmParams P) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto issue = [&](int t) {
-    char* st = smem + (t & (kStages - 1)) * kStageBytes;
-    dma_tile<A_T>(P.A, P.lda, m0, t * BK, P.M - 1, st, wid, lane);
-    dma_tile<B_T>(P.B, P.ldb, n0, t * BK, P.N - 1, st + kOpBytes, wid, lane);
-  };
-#pragma unroll
-  for (int t = 0; t < kStages - 1; ++t)
-    if (t < nk) issue(t);
+  dma_tile<A_T>(P.A, P.lda, m0, kbeg, P.M - 1, smem, wid, lane);
+  dma_tile<B_T>(P.B, P.ldb, n0, kbeg, P.N - 1, smem + kOpBytes, wid, lane);
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
 
   for (int kt = 0; kt < nk; ++kt) {
-    // retire this wave's DMAs of tile kt (4 per tile; tiles kt+1, kt+2 may stay in flight)
-    // (wait + barrier in ONE asm statement: no LDS access can be scheduled between them)
-    if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
-    else if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-    if (kt + kStages - 1 < nk) issue(kt + kStages - 1);
-    const char* As = smem + (kt & (kStages - 1)) * kStageBytes;
+    const char* As = smem + (kt & 1) * kStageBytes;
     const char* Bs = As + kOpBytes;
-    bf16x8 bf[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if constexpr (!B_T) bf[j] = frag_kc(Bs, wn * 64 + 16 * j + (lane & 15), lane >> 4);
-      else bf[j] = frag_mc(Bs, 0, wn * 64 + 16 * j, lane);
+    if (kt + 1 < nk) {
+      char* nxt = smem + ((kt + 1) & 1) * kStageBytes;
+      dma_tile<A_T>(P.A, P.lda, m0, kbeg + (kt + 1) * BK, P.M - 1, nxt, wid, lane);
+      dma_tile<B_T>(P.B, P.ldb, n0, kbeg + (kt + 1) * BK, P.N - 1, nxt + kOpBytes, wid, lane);
     }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      bf16x8 af;
-      if constexpr (!A_T) af = frag_kc(As, wm * 128 + 16 * i + (lane & 15), lane >> 4);
-      else af = frag_mc(As, 0, wm * 128 + 16 * i, lane);
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 bf[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af, acc[i][j], 0, 0, 0);
+      for (int j = 0; j < 4; ++j) {
+        if constexpr (!B_T) bf[j] = frag_kc(Bs, wn * 64 + 16 * j + (lane & 15), 4 * kk + (lane >> 4));
+        else bf[j] = frag_mc(Bs, 32 * kk, wn * 64 + 16 * j, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        bf16x8 af;
+        if constexpr (!A_T) af = frag_kc(As, wm * 128 + 16 * i + (lane & 15), 4 * kk + (lane >> 4));
+        else af = frag_mc(As, 32 * kk, wm * 128 + 16 * i, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af, acc[i][j], 0, 0, 0);
+      }
     }
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
   }
 
   // ---- epilogue from registers: acc[i][j][r] = C[m0 + wm*128 + 16i + (l&15)][n0 + wn*64 + 16j + 4(l>>4) + r]
@@ -147,32 +147,57 @@ __global__ __launch_bounds__(kThreads, 1) void gemm256_kernel(GemmParams P) {
       f32x4 v;
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * alpha + bias[j][r];
-      epilogue_store<EPI>(P, gm, gn, v);
+      if constexpr (EPI == EPI_SLAB) {  // split-K partial: plain 16-B store into slab blockIdx.y
+        float* slab = reinterpret_cast<float*>(P.C) + (size_t)blockIdx.y * P.M * P.ldc;
+        *reinterpret_cast<f32x4*>(slab + (size_t)gm * P.ldc + gn) = v;
+      } else {
+        epilogue_store<EPI>(P, gm, gn, v);
+      }
     }
   }
 }
 
 template <bool A_T, bool B_T, int EPI>
-int launch(const GemmParams& P, hipStream_t s) {
-  dim3 grid(((P.M + BM - 1) / BM) * (P.N / BN));
+int launch(const GemmParams& P, hipStream_t s, int splits) {
+  dim3 grid(((P.M + BM - 1) / BM) * (P.N / BN), splits);
   gemm256_kernel<A_T, B_T, EPI><<<grid, kThreads, 0, s>>>(P);
   return gpt2mi::check_launch("gemm256");
+}
+
+// out[i] (+)= sum_z slab[z][i]   (fixed summation order: deterministic)
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ slab, int splits, size_t n4,
+                                                            float* __restrict__ out, int accumulate) {
+  for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
+    f32x4 s = accumulate ? reinterpret_cast<const f32x4*>(out)[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int z = 0; z < splits; ++z) {
+      const f32x4 v = reinterpret_cast<const f32x4*>(slab + (size_t)z * n4 * 4)[i];
+      s[0] += v[0]; s[1] += v[1]; s[2] += v[2]; s[3] += v[3];
+    }
+    reinterpret_cast<f32x4*>(out)[i] = s;
+  }
 }
 
 }  // namespace
 
 namespace gpt2mi {
 // Layouts 0 (forward) and 1 (dgrad); N % 256 == 0, M % 64 == 0, K % 32 == 0, no split-K.
-int gemm256_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t s) {
+int gemm256_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t s, int splits) {
   switch (layout * 16 + epilogue) {
-    case 0 * 16 + EPI_BF16: return launch<false, false, EPI_BF16>(P, s);
-    case 0 * 16 + EPI_F32: return launch<false, false, EPI_F32>(P, s);
-    case 0 * 16 + EPI_RESID: return launch<false, false, EPI_RESID>(P, s);
-    case 0 * 16 + EPI_GELU: return launch<false, false, EPI_GELU>(P, s);
-    case 1 * 16 + EPI_BF16: return launch<false, true, EPI_BF16>(P, s);
-    case 1 * 16 + EPI_F32: return launch<false, true, EPI_F32>(P, s);
-    case 1 * 16 + EPI_GELU_BWD: return launch<false, true, EPI_GELU_BWD>(P, s);
+    case 0 * 16 + EPI_BF16: return launch<false, false, EPI_BF16>(P, s, 1);
+    case 0 * 16 + EPI_F32: return launch<false, false, EPI_F32>(P, s, 1);
+    case 0 * 16 + EPI_RESID: return launch<false, false, EPI_RESID>(P, s, 1);
+    case 0 * 16 + EPI_GELU: return launch<false, false, EPI_GELU>(P, s, 1);
+    case 1 * 16 + EPI_BF16: return launch<false, true, EPI_BF16>(P, s, 1);
+    case 1 * 16 + EPI_F32: return launch<false, true, EPI_F32>(P, s, 1);
+    case 1 * 16 + EPI_GELU_BWD: return launch<false, true, EPI_GELU_BWD>(P, s, 1);
+    case 2 * 16 + EPI_F32: return launch<true, true, EPI_F32>(P, s, 1);
+    case 2 * 16 + EPI_SLAB: return launch<true, true, EPI_SLAB>(P, s, splits);
     default: return -1;  // not built for this kernel: caller falls back to the 128x128 kernel
   }
+}
+
+int splitk_reduce(const float* slab, int splits, size_t n, float* out, int accumulate, hipStream_t s) {
+  splitk_reduce_kernel<<<2048, 256, 0, s>>>(slab, splits, n / 4, out, accumulate);
+  return check_launch("splitk_reduce");
 }
 }  // namespace gpt2mi

@@ -9,6 +9,7 @@ enum Epi : int {
   EPI_GELU = 3,      // aux_bf16 = u = acc+bias ; C_bf16 = drop(gelu_tanh(u))   (fc1 + NewGELU + drop1)
   EPI_GELU_BWD = 4,  // C_bf16 = drop_mask(alpha*acc) * gelu'(aux_bf16)        (fc2 dgrad -> fc1 output grad)
   EPI_ATOMIC = 5,    // atomicAdd(C_f32, alpha*acc)            (split-K wgrad into the grad arena)
+  EPI_SLAB = 6,      // split-K partial tile -> fp32 slab[blockIdx.y] (gemm256 wgrad; summed by splitk_reduce)
 };
 
 struct GemmParams {
@@ -99,5 +100,6 @@ __device__ __forceinline__ void epilogue_store(const GemmParams& P, int gm, int 
 }
 
 namespace gpt2mi {
-int gemm256_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t s);
+int gemm256_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t s, int splits);
+int splitk_reduce(const float* slab, int splits, size_t n, float* out, int accumulate, hipStream_t s);
 }

@@ -26,6 +26,7 @@ from typing import Dict, List, Optional
 import torch
 
 from . import _lib as K
+from ._lib import wgrad_splits as K_wgrad_splits
 
 BF16 = torch.bfloat16
 F32 = torch.float32
@@ -85,6 +86,10 @@ class Workspace:
         self.dU = e(M, 4 * C)
         self.dqkv = e(M, 3 * C)
         self.delta = e(B * H, T, dt=F32)
+        # split-K slabs of the 256x256 wgrad GEMMs
+        wshapes = [(3 * C, C), (C, C), (4 * C, C), (C, 4 * C)]
+        need = max(K_wgrad_splits(m, n) * m * n for m, n in wshapes) if C % 256 == 0 else 0
+        self.wgrad_ws = e(max(need, 4), dt=F32)
 
 
 class _NullCtxT:
@@ -330,6 +335,14 @@ class Engine:
         S = self.WGRAD_SPLITS
         while S > 1 and M % (64 * S) != 0:
             S //= 2
+
+        def wgrad(m, n, a, lda, b, ldb, out):
+            # dW[m][n] += dY[:, :m]^T X[:, :n] over the M tokens
+            if m % 256 == 0 and n % 256 == 0:
+                K.gemm_wgrad(m, n, M, a, lda, b, ldb, out, n, accumulate=True, workspace=ws.wgrad_ws,
+                             splits=K_wgrad_splits(m, n))
+            else:
+                K.gemm(K.WGRAD, K.EPI_ATOMIC, m, n, M, a, lda, b, ldb, out, n, splits=S)
         x = ws.x
 
         # lm_head (tied): dlnf = dlogits @ wte ; dwte (+)= dlogits^T @ lnf
@@ -338,8 +351,12 @@ class Engine:
                    alpha_dev=ws.dscale)
         wte_g = self.layout.padded_view(self.grad, "transformer.wte.weight", Vp)
         with self._probe("lm_head_wgrad"):
-            K.gemm(K.WGRAD, K.EPI_F32, Vp, C, M, ws.dlogits, Vp, ws.lnf, C, wte_g, C, alpha_dev=ws.dscale,
-                   accumulate=True)
+            if C % 256 == 0:
+                K.gemm_wgrad(Vp, C, M, ws.dlogits, Vp, ws.lnf, C, wte_g, C, accumulate=True, alpha_dev=ws.dscale,
+                             workspace=ws.wgrad_ws, splits=K_wgrad_splits(Vp, C))
+            else:
+                K.gemm(K.WGRAD, K.EPI_F32, Vp, C, M, ws.dlogits, Vp, ws.lnf, C, wte_g, C, alpha_dev=ws.dscale,
+                       accumulate=True)
         # ln_f backward starts the residual gradient; emits the fc2 branch grad of the last block
         K.layernorm_bwd(x[L], self.p("transformer.ln_f.weight"), ws.mf, ws.rf, ws.dln, ws.dres,
                         self.g("transformer.ln_f.weight"), self.g("transformer.ln_f.bias"), ws.dres_bf,
@@ -352,23 +369,19 @@ class Engine:
             # ---- MLP: dY2 = dres_bf (fc2 dropout applied), db2 done by the LN bwd above
             K.gemm(K.DGRAD, K.EPI_GELU_BWD, M, 4 * C, C, ws.dres_bf, C, self.w16(pre + "mlp.fc2.weight"), 4 * C,
                    ws.dU, 4 * C, aux=A.u, ldaux=4 * C, p_drop=pr, seed=seeds[("fc1", l)])
-            K.gemm(K.WGRAD, K.EPI_ATOMIC, C, 4 * C, M, ws.dres_bf, C, A.h, 4 * C, self.g(pre + "mlp.fc2.weight"),
-                   4 * C, splits=S)
+            wgrad(C, 4 * C, ws.dres_bf, C, A.h, 4 * C, self.g(pre + "mlp.fc2.weight"))
             K.gemm(K.DGRAD, K.EPI_BF16, M, C, 4 * C, ws.dU, 4 * C, self.w16(pre + "mlp.fc1.weight"), C, ws.dln, C)
-            K.gemm(K.WGRAD, K.EPI_ATOMIC, 4 * C, C, M, ws.dU, 4 * C, A.ln2, C, self.g(pre + "mlp.fc1.weight"), C,
-                   splits=S)
+            wgrad(4 * C, C, ws.dU, 4 * C, A.ln2, C, self.g(pre + "mlp.fc1.weight"))
             K.colsum_bf16(ws.dU, self.g(pre + "mlp.fc1.bias"), M, 4 * C, 4 * C)
             K.layernorm_bwd(A.xmid, self.p(pre + "ln2.weight"), A.m2, A.r2, ws.dln, ws.dres, self.g(pre + "ln2.weight"),
                             self.g(pre + "ln2.bias"), ws.dres_bf, self.g(pre + "attn.proj.bias"), M, C, pr,
                             seeds[("proj", l)])
             # ---- attention
             K.gemm(K.DGRAD, K.EPI_BF16, M, C, C, ws.dres_bf, C, self.w16(pre + "attn.proj.weight"), C, ws.dln, C)
-            K.gemm(K.WGRAD, K.EPI_ATOMIC, C, C, M, ws.dres_bf, C, A.ao, C, self.g(pre + "attn.proj.weight"), C,
-                   splits=S)
+            wgrad(C, C, ws.dres_bf, C, A.ao, C, self.g(pre + "attn.proj.weight"))
             K.attn_bwd(A.qkv, A.ao, ws.dln, A.lse, ws.delta, ws.dqkv, B, T, H, C // H, pa, seeds[("attn", l)])
             K.gemm(K.DGRAD, K.EPI_BF16, M, C, 3 * C, ws.dqkv, 3 * C, self.w16(pre + "attn.qkv.weight"), C, ws.dln, C)
-            K.gemm(K.WGRAD, K.EPI_ATOMIC, 3 * C, C, M, ws.dqkv, 3 * C, A.ln1, C, self.g(pre + "attn.qkv.weight"), C,
-                   splits=S)
+            wgrad(3 * C, C, ws.dqkv, 3 * C, A.ln1, C, self.g(pre + "attn.qkv.weight"))
             K.colsum_bf16(ws.dqkv, self.g(pre + "attn.qkv.bias"), M, 3 * C, 3 * C)
             if l > 0:
                 K.layernorm_bwd(x[l], self.p(pre + "ln1.weight"), A.m1, A.r1, ws.dln, ws.dres,

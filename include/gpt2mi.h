@@ -62,6 +62,14 @@ int gpt2mi_gemm(int layout, int epilogue, int M, int N, int K, const uint16_t* A
                 void* C, int ldc, const float* bias, const float* resid, uint16_t* aux, int ldaux, float alpha,
                 const float* alpha_dev, int accumulate, int splits, float p_drop, uint64_t seed, void* stream);
 
+/* Weight gradient (train_gpt2_distributed.py:412 autograd wgrad of every nn.Linear):
+ * C[M][N] (+)= alpha*(alpha_dev?) * A^T B, A stored [K][M] (dY), B stored [K][N] (X), K = tokens.
+ * 256x256 tiles; `splits` K ranges write fp32 partial slabs to `workspace` (>= splits*M*N floats),
+ * summed into C in a fixed order (deterministic). M, N multiples of 256; K of 64; ldc == N. */
+int gpt2mi_gemm_wgrad(int M, int N, int K, const uint16_t* A, int lda, const uint16_t* B, int ldb, float* C, int ldc,
+                      int accumulate, float alpha, const float* alpha_dev, float* workspace, size_t workspace_floats,
+                      int splits, void* stream);
+
 /* K4-K8: causal flash attention, head_dim 64 — model.py:124-155. q/k/v read from qkv [B*T, 3C];
  * out [B*T, C] head-merged; lse [B*H, T] (natural log of the 1/sqrt(D)-scaled scores). */
 int gpt2mi_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int T, int H, int head_dim, float p_drop,

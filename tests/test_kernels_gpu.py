@@ -359,3 +359,18 @@ def test_gemm256_matches_gemm128(layout, epi):
     L().set_gemm_impl(0)
     assert rel_err(outs[0][0], outs[1][0]) < 1e-5 if epi == 2 else rel_err(outs[0][0], outs[1][0]) < 2e-3
     assert rel_err(outs[0][1], outs[1][1]) < 2e-3
+
+
+@pytest.mark.parametrize("M,N,K,splits", [(256, 256, 1024, 1), (512, 768, 4096, 7), (768, 256, 2048, 3)])
+def test_gemm_wgrad_splitk_slabs(M, N, K, splits):
+    g = torch.Generator().manual_seed(M + N + splits)
+    A, B = bf(torch.randn(K, M, generator=g)), bf(torch.randn(K, N, generator=g))
+    C0 = torch.randn(M, N, generator=g)
+    C = C0.to(dev)
+    ws = torch.empty(splits * M * N, device=dev)
+    L().gemm_wgrad(M, N, K, A.to(dev), M, B.to(dev), N, C, N, accumulate=True, alpha=0.5, workspace=ws, splits=splits)
+    assert rel_err(C.cpu(), C0 + 0.5 * (A.float().t() @ B.float())) < 1e-5
+    # deterministic: same inputs -> bitwise same result
+    C2 = C0.to(dev)
+    L().gemm_wgrad(M, N, K, A.to(dev), M, B.to(dev), N, C2, N, accumulate=True, alpha=0.5, workspace=ws, splits=splits)
+    assert torch.equal(C, C2)

@@ -56,6 +56,8 @@ def gemm(M=65536):
         ("qkv dgrad", 1, K.EPI_BF16, M, C, 3 * C),
         ("lm dgrad", 1, K.EPI_BF16, M, C, 50432),
         ("fc1 wgrad", 2, K.EPI_ATOMIC, 4 * C, C, M),
+        ("fc2 wgrad", 2, K.EPI_ATOMIC, C, 4 * C, M),
+        ("proj wgrad", 2, K.EPI_ATOMIC, C, C, M),
         ("qkv wgrad", 2, K.EPI_ATOMIC, 3 * C, C, M),
         ("lm wgrad", 2, K.EPI_F32, 50432, C, M),
     ]
@@ -75,8 +77,13 @@ def gemm(M=65536):
         resid = torch.zeros(m, n, device=dev) if epi == K.EPI_RESID else None
         aux = torch.zeros(m, n, device=dev, dtype=torch.bfloat16) if epi in (K.EPI_GELU, K.EPI_GELU_BWD) else None
         splits = 4 if epi == K.EPI_ATOMIC else 1
-        fn = lambda: K.gemm(lay, epi, m, n, k, A, lda, Bm, ldb, Cm, n, bias=bias if lay == 0 else None,  # noqa
-                            resid=resid, aux=aux, ldaux=n, splits=splits)
+        if lay == 2 and m % 256 == 0:
+            sp = K.wgrad_splits(m, n)
+            wsb = torch.empty(max(4, sp * m * n if sp > 1 else 4), device=dev)
+            fn = lambda: K.gemm_wgrad(m, n, k, A, lda, Bm, ldb, Cm, n, workspace=wsb, splits=sp)  # noqa
+        else:
+            fn = lambda: K.gemm(lay, epi, m, n, k, A, lda, Bm, ldb, Cm, n, bias=bias if lay == 0 else None,  # noqa
+                                resid=resid, aux=aux, ldaux=n, splits=splits)
         ms = timeit(fn, reps=10)
         tf = 2.0 * m * n * k / ms / 1e9
         print(f"{name:16s} M={m:6d} N={n:6d} K={k:6d}: {ms:7.3f} ms {tf:6.0f} TF ({tf/PEAK*100:4.1f}%)")
@@ -99,7 +106,7 @@ if __name__ == "__main__":
         attn(p=0.1)
     if "gemm" in what:
         for impl in (0, 1):
-            print(f"--- gemm impl {impl} ({'auto: 256x256 for fwd/dgrad' if impl == 0 else '128x128 only'})")
+            print(f"--- gemm impl {impl} ({ {0: '256x256 where it applies', 1: '128x128 only'}[impl] })")
             K.set_gemm_impl(impl)
             gemm()
         K.set_gemm_impl(0)
