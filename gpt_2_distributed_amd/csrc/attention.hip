@@ -80,9 +80,8 @@ __device__ __forceinline__ void tile_store(char* base, const u32x4* r) {
   }
 }
 
-__device__ __forceinline__ uint64_t att_idx(int bh, int T, int q, int k) {
-  return ((uint64_t)bh * T + q) * T + k;
-}
+// Dropout of attention probability (q, key) of head bh: 16-bit half (q >> 4) & 1 of
+// drop_hash(seed, (bh*T + (q & ~16))*T + key) — queries q and q^16 of one key share a hash.
 
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
@@ -146,33 +145,33 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const bf16* __res
           s[1][fi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[1][kk], s[1][fi], 0, 0, 0);
         }
       }
+      if (diag) {  // causal mask only on the diagonal tiles (wave-uniform branch)
+#pragma unroll
+        for (int qg = 0; qg < 2; ++qg)
+#pragma unroll
+          for (int fi = 0; fi < 4; ++fi)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (k_lo + 16 * fi + 4 * g + r > q_lo + 16 * qg + (lane & 15)) s[qg][fi][r] = -INFINITY;
+      }
 #pragma unroll
       for (int qg = 0; qg < 2; ++qg) {
-        const int q = q_lo + 16 * qg + (lane & 15);
-        float tmax = -INFINITY;
+        float tmax = -INFINITY;  // max of the raw scores (scale > 0)
 #pragma unroll
         for (int fi = 0; fi < 4; ++fi)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float t = s[qg][fi][r] * sl2;
-            if (diag && (k_lo + 16 * fi + 4 * g + r) > q) t = -INFINITY;
-            s[qg][fi][r] = t;
-            tmax = fmaxf(tmax, t);
-          }
+          tmax = fmaxf(tmax, fmaxf(fmaxf(s[qg][fi][0], s[qg][fi][1]), fmaxf(s[qg][fi][2], s[qg][fi][3])));
         tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
         tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-        const float mn = fmaxf(m[qg], tmax);  // finite: tile 0 holds key 0, visible to every query
+        const float mn = fmaxf(m[qg], tmax * sl2);  // finite: tile 0 holds key 0, visible to every query
         const float corr = exp2f(m[qg] - mn);
         float rs = 0.f;
 #pragma unroll
         for (int fi = 0; fi < 4; ++fi)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float p = exp2f(s[qg][fi][r] - mn);
+            const float p = exp2f(fmaf(s[qg][fi][r], sl2, -mn));
             rs += p;
-            float pd = p;
-            if (thr) pd = drop_keep(seed, att_idx(bh, T, q, k_lo + 16 * fi + 4 * g + r), thr) ? p * inv_keep : 0.f;
-            s[qg][fi][r] = pd;
+            s[qg][fi][r] = p;
           }
         rs += __shfl_xor(rs, 16, 64);
         rs += __shfl_xor(rs, 32, 64);
@@ -182,6 +181,18 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const bf16* __res
         for (int f = 0; f < 4; ++f)
 #pragma unroll
           for (int r = 0; r < 4; ++r) o[qg][f][r] *= corr;
+      }
+      if (thr) {  // dropout on P (not on the normaliser): one hash per (q, q^16) pair of a key
+        const uint32_t s32 = seed32(seed);
+        const uint32_t pbase = ((uint32_t)bh * T + q_lo + (lane & 15)) * (uint32_t)T + k_lo + 4 * g;
+#pragma unroll
+        for (int fi = 0; fi < 4; ++fi)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const uint32_t hh = drop_hash(s32, pbase + 16 * fi + r);
+            s[0][fi][r] = drop_keep16(hh, 0, thr) ? s[0][fi][r] * inv_keep : 0.f;
+            s[1][fi][r] = drop_keep16(hh, 1, thr) ? s[1][fi][r] * inv_keep : 0.f;
+          }
       }
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
@@ -307,20 +318,28 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const bf16* __
           }
         }
       }
-#pragma unroll
-      for (int qg = 0; qg < 2; ++qg) {
-        const int q = q_lo + 16 * qg + (lane & 15);
+      if (thr) {  // dropped entries get dP = 0 (same (q, q^16)-pair hash as the forward)
+        const uint32_t s32 = seed32(seed);
+        const uint32_t pbase = ((uint32_t)bh * T + q_lo + (lane & 15)) * (uint32_t)T + k_lo + 4 * g;
 #pragma unroll
         for (int fi = 0; fi < 4; ++fi)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int key = k_lo + 16 * fi + 4 * g + r;
-            const float p = (diag && key > q) ? 0.f : exp2f(s[qg][fi][r] * sl2 - lse2[qg]);
-            float d = dp[qg][fi][r];
-            if (thr) d = drop_keep(seed, att_idx(bh, T, q, key), thr) ? d * inv_keep : 0.f;
-            s[qg][fi][r] = p * (d - dl[qg]);  // dS^T
+            const uint32_t hh = drop_hash(s32, pbase + 16 * fi + r);
+            dp[0][fi][r] = drop_keep16(hh, 0, thr) ? dp[0][fi][r] * inv_keep : 0.f;
+            dp[1][fi][r] = drop_keep16(hh, 1, thr) ? dp[1][fi][r] * inv_keep : 0.f;
           }
       }
+#pragma unroll
+      for (int qg = 0; qg < 2; ++qg)
+#pragma unroll
+        for (int fi = 0; fi < 4; ++fi)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float p = exp2f(fmaf(s[qg][fi][r], sl2, -lse2[qg]));
+            if (diag && k_lo + 16 * fi + 4 * g + r > q_lo + 16 * qg + (lane & 15)) p = 0.f;
+            s[qg][fi][r] = p * (dp[qg][fi][r] - dl[qg]);  // dS^T
+          }
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         const bf16x8 s0 = pack_perm(s[0], kk), s1 = pack_perm(s[1], kk);
@@ -440,27 +459,37 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(const bf16* 
         }
       }
       // s[kg][fi][r] = S[q = q0 + 16fi + 4g + r][key = k_lo + 16kg + (l&15)]
+      f32x4 l4[4], d4[4];
 #pragma unroll
       for (int fi = 0; fi < 4; ++fi) {
-        const f32x4 l4 = *reinterpret_cast<const f32x4*>(Ls + 16 * fi + 4 * g);
-        const f32x4 d4 = *reinterpret_cast<const f32x4*>(Dl + 16 * fi + 4 * g);
+        l4[fi] = *reinterpret_cast<const f32x4*>(Ls + 16 * fi + 4 * g);
+        d4[fi] = *reinterpret_cast<const f32x4*>(Dl + 16 * fi + 4 * g);
+      }
+      const uint32_t s32 = seed32(seed);
 #pragma unroll
-        for (int kg = 0; kg < 2; ++kg) {
-          const int key = k_lo + 16 * kg + (lane & 15);
+      for (int kg = 0; kg < 2; ++kg) {
+        const int key = k_lo + 16 * kg + (lane & 15);
+#pragma unroll
+        for (int fp = 0; fp < 2; ++fp)  // queries q and q^16 (fi = 2fp, 2fp+1) share one dropout hash
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int qq = q0 + 16 * fi + 4 * g + r;
-            const float p = (diag && qq < key) ? 0.f : exp2f(s[kg][fi][r] * sl2 - l4[r]);
-            float pdv = p, d = dp[kg][fi][r];
-            if (thr) {
-              const bool keep = drop_keep(seed, att_idx(bh, T, qq, key), thr);
-              pdv = keep ? p * inv_keep : 0.f;
-              d = keep ? d * inv_keep : 0.f;
+            uint32_t hh = 0;
+            if (thr) hh = drop_hash(s32, ((uint32_t)bh * T + q0 + 32 * fp + 4 * g + r) * (uint32_t)T + key);
+#pragma unroll
+            for (int half = 0; half < 2; ++half) {
+              const int fi = 2 * fp + half;
+              float p = exp2f(fmaf(s[kg][fi][r], sl2, -l4[fi][r]));
+              if (diag && q0 + 16 * fi + 4 * g + r < key) p = 0.f;
+              float pdv = p, d = dp[kg][fi][r];
+              if (thr) {
+                const bool keep = drop_keep16(hh, half, thr);
+                pdv = keep ? p * inv_keep : 0.f;
+                d = keep ? d * inv_keep : 0.f;
+              }
+              dp[kg][fi][r] = pdv;                  // dropped P (for dV)
+              s[kg][fi][r] = p * (d - d4[fi][r]);   // dS
             }
-            dp[kg][fi][r] = pdv;               // dropped P (for dV)
-            s[kg][fi][r] = p * (d - d4[r]);    // dS
           }
-        }
       }
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {

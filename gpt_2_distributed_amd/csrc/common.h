@@ -49,27 +49,32 @@ __device__ __forceinline__ float wave_max(float v) {
 
 // ---- counter-based dropout RNG -------------------------------------------------------------------
 // keep(i) is a pure function of (seed, element index), so backward regenerates the forward mask
-// without storing it. 32-bit multiply-xorshift finaliser (the element index of every dropout site
-// fits in 32 bits: attention B*H*T*T < 2^32 for every BASELINE config); 24 random bits compared to
-// p*2^24. ~8 VALU ops per element (a 64-bit mixer cost 3-4x that inside the attention loop).
-__device__ __forceinline__ uint32_t drop_bits(uint64_t seed, uint64_t idx) {
-  uint32_t h = (uint32_t)idx * 0x9E3779B1u + ((uint32_t)seed ^ (uint32_t)(seed >> 32));
+// without storing it. One 32-bit multiply-xorshift hash yields TWO 16-bit uniforms: element pairs
+// share a hash (GEMM/LN/embedding sites: elements 2j, 2j+1; attention: queries q, q^16 of one key,
+// which sit in the same lane in every attention kernel). keep = uniform16 >= round(p * 2^16).
+// All element / pair indices fit in 32 bits for every BASELINE config (attention B*H*T*T < 2^32).
+__device__ __forceinline__ uint32_t seed32(uint64_t seed) { return (uint32_t)seed ^ (uint32_t)(seed >> 32); }
+__device__ __forceinline__ uint32_t drop_hash(uint32_t s32, uint32_t x) {
+  uint32_t h = x * 0x9E3779B1u + s32;
   h ^= h >> 15;
   h *= 0x2C1B3C6Du;
   h ^= h >> 12;
   h *= 0x297A2D39u;
   h ^= h >> 15;
-  return h >> 8;
+  return h;
 }
-// threshold = (uint32)(p * 2^24); keep if bits >= threshold.
+__device__ __forceinline__ bool drop_keep16(uint32_t h, int half, uint32_t thr) {
+  return ((half ? (h >> 16) : h) & 0xFFFFu) >= thr;
+}
+// element-indexed form: element i uses half (i & 1) of hash(i >> 1)
 __device__ __forceinline__ bool drop_keep(uint64_t seed, uint64_t idx, uint32_t thr) {
-  return drop_bits(seed, idx) >= thr;
+  return drop_keep16(drop_hash(seed32(seed), (uint32_t)(idx >> 1)), (int)(idx & 1), thr);
 }
 
 static inline uint32_t drop_threshold(float p) {
   if (p <= 0.f) return 0u;
-  double t = (double)p * 16777216.0;
-  return (uint32_t)(t > 16777216.0 ? 16777216.0 : t);
+  double t = (double)p * 65536.0 + 0.5;
+  return (uint32_t)(t > 65536.0 ? 65536.0 : t);
 }
 
 // ---- XCD-aware block remap (blocks b and b+8 share an XCD; give each XCD a contiguous range) ----

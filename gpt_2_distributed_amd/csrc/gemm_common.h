@@ -44,10 +44,23 @@ __device__ __forceinline__ float gelu_grad_f(float u) {
 }
 
 // Apply the fused epilogue to 4 consecutive outputs C[gm][gn..gn+3]; v = alpha*acc (+bias).
+// keep mask of the 4 dropout elements didx..didx+3 (didx even): two hashes, 16 bits per element
+__device__ __forceinline__ void drop4(const GemmParams& P, uint64_t didx, bool keep[4]) {
+  const uint32_t s = seed32(P.seed);
+  const uint32_t h0 = drop_hash(s, (uint32_t)(didx >> 1)), h1 = drop_hash(s, (uint32_t)(didx >> 1) + 1u);
+  keep[0] = drop_keep16(h0, 0, P.thr);
+  keep[1] = drop_keep16(h0, 1, P.thr);
+  keep[2] = drop_keep16(h1, 0, P.thr);
+  keep[3] = drop_keep16(h1, 1, P.thr);
+}
+
 template <int EPI>
 __device__ __forceinline__ void epilogue_store(const GemmParams& P, int gm, int gn, f32x4 v) {
   const size_t cidx = (size_t)gm * P.ldc + gn;
-  const uint64_t didx = (uint64_t)gm * P.N + gn;  // dropout element index in the logical [M,N]
+  const uint64_t didx = (uint64_t)gm * P.N + gn;  // dropout element index in the logical [M,N] (even)
+  bool keep[4] = {true, true, true, true};
+  if (EPI == EPI_RESID || EPI == EPI_GELU || EPI == EPI_GELU_BWD)
+    if (P.thr) drop4(P, didx, keep);
   if constexpr (EPI == EPI_BF16) {
     bf16* C = reinterpret_cast<bf16*>(P.C);
     *reinterpret_cast<bf16x4*>(C + cidx) = bf16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
@@ -65,7 +78,7 @@ __device__ __forceinline__ void epilogue_store(const GemmParams& P, int gm, int 
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       float y = v[j];
-      if (P.thr) y = drop_keep(P.seed, didx + j, P.thr) ? y * P.inv_keep : 0.f;
+      if (P.thr) y = keep[j] ? y * P.inv_keep : 0.f;
       r[j] += y;
     }
     *reinterpret_cast<f32x4*>(C + cidx) = r;
@@ -76,7 +89,7 @@ __device__ __forceinline__ void epilogue_store(const GemmParams& P, int gm, int 
     for (int j = 0; j < 4; ++j) {
       u[j] = f2bf(v[j]);
       float a = gelu_f(v[j]);
-      if (P.thr) a = drop_keep(P.seed, didx + j, P.thr) ? a * P.inv_keep : 0.f;
+      if (P.thr) a = keep[j] ? a * P.inv_keep : 0.f;
       h[j] = f2bf(a);
     }
     *reinterpret_cast<bf16x4*>(P.aux + (size_t)gm * P.ldaux + gn) = u;
@@ -88,7 +101,7 @@ __device__ __forceinline__ void epilogue_store(const GemmParams& P, int gm, int 
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       float d = v[j];
-      if (P.thr) d = drop_keep(P.seed, didx + j, P.thr) ? d * P.inv_keep : 0.f;
+      if (P.thr) d = keep[j] ? d * P.inv_keep : 0.f;
       o[j] = f2bf(d * gelu_grad_f(bf2f(u[j])));
     }
     *reinterpret_cast<bf16x4*>(C + cidx) = o;
