@@ -373,7 +373,7 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const bf16* __
 
 // ---------------------------------------------------------------------------------------------
 // dK, dV: key-outer (128 keys per workgroup, 32 per wave) over 64-query tiles at or after the keys.
-__global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(const bf16* __restrict__ qkv,
+__global__ __launch_bounds__(kThreads, 2) void attn_bwd_dkdv_kernel(const bf16* __restrict__ qkv,
                                                                     const bf16* __restrict__ dout,
                                                                     const float* __restrict__ lse,
                                                                     const float* __restrict__ delta,
@@ -443,67 +443,67 @@ __global__ __launch_bounds__(kThreads, 1) void attn_bwd_dkdv_kernel(const bf16* 
     const int q0 = i * BQT;
     if (wave_valid && q0 + BQT - 1 >= k_lo) {  // wave-uniform: a query of the tile sees a key of the wave
       const bool diag = q0 < k_lo + 31;
-      f32x4 s[2][4], dp[2][4];
+      const uint32_t s32 = seed32(seed);
+      // Two 32-query halves per 64-query tile; each half is exactly one MFMA k-step of the dV/dK
+      // products, so only half of S / dP is live at a time (register pressure -> occupancy).
 #pragma unroll
-      for (int fi = 0; fi < 4; ++fi) {
-        s[0][fi] = s[1][fi] = dp[0][fi] = dp[1][fi] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int hq = 0; hq < 2; ++hq) {
+        f32x4 s[2][2], dp[2][2];  // [kg][fl]: S[q = q0 + 16(2hq+fl) + 4g + r][key = k_lo + 16kg + (l&15)]
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-          const bf16x8 qa = row_frag(Qs, 16 * fi, kk, lane);
-          const bf16x8 da = row_frag(Ds, 16 * fi, kk, lane);
+        for (int fl = 0; fl < 2; ++fl) {
+          const int fi = 2 * hq + fl;
+          s[0][fl] = s[1][fl] = dp[0][fl] = dp[1][fl] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int kg = 0; kg < 2; ++kg) {
-            s[kg][fi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[kg][kk], s[kg][fi], 0, 0, 0);
-            dp[kg][fi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, vf[kg][kk], dp[kg][fi], 0, 0, 0);
+          for (int kk = 0; kk < 2; ++kk) {
+            const bf16x8 qa = row_frag(Qs, 16 * fi, kk, lane);
+            const bf16x8 da = row_frag(Ds, 16 * fi, kk, lane);
+#pragma unroll
+            for (int kg = 0; kg < 2; ++kg) {
+              s[kg][fl] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[kg][kk], s[kg][fl], 0, 0, 0);
+              dp[kg][fl] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, vf[kg][kk], dp[kg][fl], 0, 0, 0);
+            }
           }
         }
-      }
-      // s[kg][fi][r] = S[q = q0 + 16fi + 4g + r][key = k_lo + 16kg + (l&15)]
-      f32x4 l4[4], d4[4];
+        f32x4 l4[2], d4[2];
 #pragma unroll
-      for (int fi = 0; fi < 4; ++fi) {
-        l4[fi] = *reinterpret_cast<const f32x4*>(Ls + 16 * fi + 4 * g);
-        d4[fi] = *reinterpret_cast<const f32x4*>(Dl + 16 * fi + 4 * g);
-      }
-      const uint32_t s32 = seed32(seed);
+        for (int fl = 0; fl < 2; ++fl) {
+          l4[fl] = *reinterpret_cast<const f32x4*>(Ls + 16 * (2 * hq + fl) + 4 * g);
+          d4[fl] = *reinterpret_cast<const f32x4*>(Dl + 16 * (2 * hq + fl) + 4 * g);
+        }
 #pragma unroll
-      for (int kg = 0; kg < 2; ++kg) {
-        const int key = k_lo + 16 * kg + (lane & 15);
-#pragma unroll
-        for (int fp = 0; fp < 2; ++fp)  // queries q and q^16 (fi = 2fp, 2fp+1) share one dropout hash
+        for (int kg = 0; kg < 2; ++kg) {
+          const int key = k_lo + 16 * kg + (lane & 15);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            uint32_t hh = 0;
-            if (thr) hh = drop_hash(s32, ((uint32_t)bh * T + q0 + 32 * fp + 4 * g + r) * (uint32_t)T + key);
+            uint32_t hh = 0;  // queries q and q^16 (fl = 0, 1) share one dropout hash
+            if (thr) hh = drop_hash(s32, ((uint32_t)bh * T + q0 + 32 * hq + 4 * g + r) * (uint32_t)T + key);
 #pragma unroll
-            for (int half = 0; half < 2; ++half) {
-              const int fi = 2 * fp + half;
-              float p = exp2f(fmaf(s[kg][fi][r], sl2, -l4[fi][r]));
-              if (diag && q0 + 16 * fi + 4 * g + r < key) p = 0.f;
-              float pdv = p, d = dp[kg][fi][r];
+            for (int fl = 0; fl < 2; ++fl) {
+              float p = exp2f(fmaf(s[kg][fl][r], sl2, -l4[fl][r]));
+              if (diag && q0 + 16 * (2 * hq + fl) + 4 * g + r < key) p = 0.f;
+              float pdv = p, d = dp[kg][fl][r];
               if (thr) {
-                const bool keep = drop_keep16(hh, half, thr);
+                const bool keep = drop_keep16(hh, fl, thr);
                 pdv = keep ? p * inv_keep : 0.f;
                 d = keep ? d * inv_keep : 0.f;
               }
-              dp[kg][fi][r] = pdv;                  // dropped P (for dV)
-              s[kg][fi][r] = p * (d - d4[fi][r]);   // dS
+              dp[kg][fl][r] = pdv;                 // dropped P (for dV)
+              s[kg][fl][r] = p * (d - d4[fl][r]);  // dS
             }
           }
-      }
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const bf16x8 p0 = pack_perm(dp[0], kk), p1 = pack_perm(dp[1], kk);
-        const bf16x8 s0 = pack_perm(s[0], kk), s1 = pack_perm(s[1], kk);
+        }
+        const bf16x8 p0 = pack_perm(dp[0], 0), p1 = pack_perm(dp[1], 0);
+        const bf16x8 s0 = pack_perm(s[0], 0), s1 = pack_perm(s[1], 0);
 #pragma unroll
         for (int fd = 0; fd < 4; ++fd) {
-          const bf16x8 dot = tr_frag(Ds, kk, 16 * fd, lane);
-          const bf16x8 qt = tr_frag(Qs, kk, 16 * fd, lane);
+          const bf16x8 dot = tr_frag(Ds, hq, 16 * fd, lane);
+          const bf16x8 qt = tr_frag(Qs, hq, 16 * fd, lane);
           dv[0][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dot, p0, dv[0][fd], 0, 0, 0);
           dv[1][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dot, p1, dv[1][fd], 0, 0, 0);
           dk[0][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qt, s0, dk[0][fd], 0, 0, 0);
           dk[1][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qt, s1, dk[1][fd], 0, 0, 0);
         }
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
     if (i + 1 < nqt) sstore(smem + (cur ^ 1) * kStage);
