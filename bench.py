@@ -70,9 +70,9 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    from gpt_2_distributed_amd.parallel import init_distributed, local_device_index
+    local_rank = local_device_index()
     if world > 1:
-        from gpt_2_distributed_amd.parallel import init_distributed
         init_distributed()
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)

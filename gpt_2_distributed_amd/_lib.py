@@ -131,10 +131,12 @@ def gemm_wgrad(M, N, K, A, lda, B, ldb, C, ldc, accumulate=True, alpha=1.0, alph
           _ptr(alpha_dev), _ptr(workspace), ws_n, splits, _stream())
 
 
-def wgrad_splits(M, N, cus=256):
-    """Split-K factor for a wgrad output of M x N on 256x256 tiles: fill one wave of the 256 CUs."""
+def wgrad_splits(M, N, K, cus=256):
+    """Split-K factor for a wgrad output of M x N (K tokens) on 256x256 tiles: fill one wave of the
+    256 CUs, at least 4 K-tiles (of 64) per split."""
     tiles = (M // 256) * (N // 256)
-    return 1 if tiles >= cus else max(1, cus // tiles)
+    s = 1 if tiles >= cus else max(1, cus // tiles)
+    return max(1, min(s, K // 256))
 
 
 def attn_fwd(qkv, out, lse, B, T, H, D, p_drop=0.0, seed=0):

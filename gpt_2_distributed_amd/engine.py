@@ -87,8 +87,9 @@ class Workspace:
         self.dqkv = e(M, 3 * C)
         self.delta = e(B * H, T, dt=F32)
         # split-K slabs of the 256x256 wgrad GEMMs
-        wshapes = [(3 * C, C), (C, C), (4 * C, C), (C, 4 * C)]
-        need = max(K_wgrad_splits(m, n) * m * n for m, n in wshapes) if C % 256 == 0 else 0
+        wshapes = [(3 * C, C), (C, C), (4 * C, C), (C, 4 * C), (vpad, C)]
+        need = max((K_wgrad_splits(m, n, M) * m * n if K_wgrad_splits(m, n, M) > 1 else 0)
+                   for m, n in wshapes) if C % 256 == 0 else 0
         self.wgrad_ws = e(max(need, 4), dt=F32)
 
 
@@ -340,7 +341,7 @@ class Engine:
             # dW[m][n] += dY[:, :m]^T X[:, :n] over the M tokens
             if m % 256 == 0 and n % 256 == 0:
                 K.gemm_wgrad(m, n, M, a, lda, b, ldb, out, n, accumulate=True, workspace=ws.wgrad_ws,
-                             splits=K_wgrad_splits(m, n))
+                             splits=K_wgrad_splits(m, n, M))
             else:
                 K.gemm(K.WGRAD, K.EPI_ATOMIC, m, n, M, a, lda, b, ldb, out, n, splits=S)
         x = ws.x
@@ -353,7 +354,7 @@ class Engine:
         with self._probe("lm_head_wgrad"):
             if C % 256 == 0:
                 K.gemm_wgrad(Vp, C, M, ws.dlogits, Vp, ws.lnf, C, wte_g, C, accumulate=True, alpha_dev=ws.dscale,
-                             workspace=ws.wgrad_ws, splits=K_wgrad_splits(Vp, C))
+                             workspace=ws.wgrad_ws, splits=K_wgrad_splits(Vp, C, M))
             else:
                 K.gemm(K.WGRAD, K.EPI_F32, Vp, C, M, ws.dlogits, Vp, ws.lnf, C, wte_g, C, alpha_dev=ws.dscale,
                        accumulate=True)

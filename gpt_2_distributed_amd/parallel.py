@@ -31,14 +31,23 @@ import torch
 import torch.distributed as dist
 
 
+def local_device_index() -> int:
+    """LOCAL_RANK -> device (train_gpt2_distributed.py:59). GPT2MI_SINGLE_DEVICE=1 puts every rank on
+    device 0: a test hook to rehearse the multi-rank path on a one-GPU box (with a gloo backend)."""
+    if os.environ.get("GPT2MI_SINGLE_DEVICE") == "1":
+        return 0
+    return int(os.environ.get("LOCAL_RANK", 0))
+
+
 def init_distributed() -> None:
-    """train_gpt2_distributed.py:50-59."""
+    """train_gpt2_distributed.py:50-59: init_process_group("nccl") (= RCCL) + set_device(LOCAL_RANK).
+    GPT2MI_DIST_BACKEND overrides the backend (tests)."""
     if dist.is_initialized():
         return
-    backend = "nccl" if torch.cuda.is_available() else "gloo"
+    backend = os.environ.get("GPT2MI_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     dist.init_process_group(backend)
     if torch.cuda.is_available():
-        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", 0)))
+        torch.cuda.set_device(local_device_index())
 
 
 def is_primary() -> bool:

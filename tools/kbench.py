@@ -78,7 +78,7 @@ def gemm(M=65536):
         aux = torch.zeros(m, n, device=dev, dtype=torch.bfloat16) if epi in (K.EPI_GELU, K.EPI_GELU_BWD) else None
         splits = 4 if epi == K.EPI_ATOMIC else 1
         if lay == 2 and m % 256 == 0:
-            sp = K.wgrad_splits(m, n)
+            sp = K.wgrad_splits(m, n, k)
             wsb = torch.empty(max(4, sp * m * n if sp > 1 else 4), device=dev)
             fn = lambda: K.gemm_wgrad(m, n, k, A, lda, Bm, ldb, Cm, n, workspace=wsb, splits=sp)  # noqa
         else:
