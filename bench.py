@@ -101,7 +101,8 @@ def main():
 
     def step(i):
         x, y = batches[i % len(batches)]
-        _, loss = fwd(x, labels=y)
+        with torch.autocast("cuda", dtype=torch.bfloat16):  # the reference trainer's step (:404)
+            _, loss = fwd(x, labels=y)
         loss.backward()
         opt.step()
         opt.zero_grad()

@@ -39,6 +39,14 @@ _SIGS = {
     "gpt2mi_scale_mul": [_p, _p, _p, _p],
     "gpt2mi_memset_zero": [_p, _c_size, _p],
     "gpt2mi_set_gemm_impl": [_c_int],
+    "gpt2mi_gemm_f32": [_c_int, _c_int, _c_int, _c_int, _c_int, _p, _c_int, _p, _c_int, _p, _c_int, _p, _p, _p,
+                        _c_int, _c_float, _p, _c_int, _c_int, _c_float, _c_u64, _p],
+    "gpt2mi_attn_fwd_f32": [_p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_float, _c_u64, _p],
+    "gpt2mi_attn_bwd_f32": [_p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_float, _c_u64, _p],
+    "gpt2mi_layernorm_bwd_f32": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_float, _c_u64, _c_int,
+                                 _p],
+    "gpt2mi_colsum_f32": [_p, _p, _c_int, _c_int, _c_int, _p],
+    "gpt2mi_xent_fwd_f32": [_p, _c_int, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _p, _p, _p],
     "gpt2mi_gemm_wgrad": [_c_int, _c_int, _c_int, _p, _c_int, _p, _c_int, _p, _c_int, _c_int, _c_float, _p, _p,
                           _c_size, _c_int, _p],
 }
@@ -82,6 +90,17 @@ def _stream():
     return torch.cuda.current_stream().cuda_stream
 
 
+def _f32(t: Optional[torch.Tensor]) -> bool:
+    """Activation dtype selects the kernel family: fp32 tensors -> the fp32 (no-autocast) kernels."""
+    if t is None:
+        return False
+    if t.dtype == torch.float32:
+        return True
+    if t.dtype != torch.bfloat16:
+        raise KernelError(f"gpt2mi kernels take bf16 or fp32 activations (got {t.dtype})")
+    return False
+
+
 def _call(name: str, *args):
     lib = load()
     rc = getattr(lib, name)(*args)
@@ -104,23 +123,26 @@ def embed_bwd(idx, dres, dwte, dwpe, B, T, C, p=0.0, seed=0):
 
 
 def layernorm_fwd(x, w, b, y_bf16, y_f32, mean, rstd, M, C, eps):
+    if y_bf16 is not None and _f32(y_bf16):  # fp32 mode: the GEMM-operand output is fp32
+        y_bf16, y_f32 = None, y_bf16
     _call("gpt2mi_layernorm_fwd", _ptr(x), _ptr(w), _ptr(b), _ptr(y_bf16), _ptr(y_f32), _ptr(mean), _ptr(rstd),
           M, C, eps, _stream())
 
 
 def layernorm_bwd(x, w, mean, rstd, dy, dres, dw, db, out_bf16, dbias_out, M, C, p_out=0.0, seed_out=0,
                   dres_init=False):
-    _call("gpt2mi_layernorm_bwd", _ptr(x), _ptr(w), _ptr(mean), _ptr(rstd), _ptr(dy), _ptr(dres), _ptr(dw),
+    name = "gpt2mi_layernorm_bwd_f32" if _f32(dy) else "gpt2mi_layernorm_bwd"
+    _call(name, _ptr(x), _ptr(w), _ptr(mean), _ptr(rstd), _ptr(dy), _ptr(dres), _ptr(dw),
           _ptr(db), _ptr(out_bf16), _ptr(dbias_out), M, C, p_out, seed_out, int(dres_init), _stream())
 
 
 def colsum_bf16(g, db, M, N, ld):
-    _call("gpt2mi_colsum_bf16", _ptr(g), _ptr(db), M, N, ld, _stream())
+    _call("gpt2mi_colsum_f32" if _f32(g) else "gpt2mi_colsum_bf16", _ptr(g), _ptr(db), M, N, ld, _stream())
 
 
 def gemm(layout, epilogue, M, N, K, A, lda, B, ldb, C, ldc, bias=None, resid=None, aux=None, ldaux=0,
          alpha=1.0, alpha_dev=None, accumulate=False, splits=1, p_drop=0.0, seed=0):
-    _call("gpt2mi_gemm", layout, epilogue, M, N, K, _ptr(A), lda, _ptr(B), ldb, _ptr(C), ldc, _ptr(bias),
+    _call("gpt2mi_gemm_f32" if _f32(A) else "gpt2mi_gemm", layout, epilogue, M, N, K, _ptr(A), lda, _ptr(B), ldb, _ptr(C), ldc, _ptr(bias),
           _ptr(resid), _ptr(aux), ldaux, alpha, _ptr(alpha_dev), int(accumulate), splits, p_drop, seed, _stream())
 
 
@@ -140,16 +162,16 @@ def wgrad_splits(M, N, K, cus=256):
 
 
 def attn_fwd(qkv, out, lse, B, T, H, D, p_drop=0.0, seed=0):
-    _call("gpt2mi_attn_fwd", _ptr(qkv), _ptr(out), _ptr(lse), B, T, H, D, p_drop, seed, _stream())
+    _call("gpt2mi_attn_fwd_f32" if _f32(qkv) else "gpt2mi_attn_fwd", _ptr(qkv), _ptr(out), _ptr(lse), B, T, H, D, p_drop, seed, _stream())
 
 
 def attn_bwd(qkv, out, dout, lse, delta, dqkv, B, T, H, D, p_drop=0.0, seed=0):
-    _call("gpt2mi_attn_bwd", _ptr(qkv), _ptr(out), _ptr(dout), _ptr(lse), _ptr(delta), _ptr(dqkv), B, T, H, D,
+    _call("gpt2mi_attn_bwd_f32" if _f32(qkv) else "gpt2mi_attn_bwd", _ptr(qkv), _ptr(out), _ptr(dout), _ptr(lse), _ptr(delta), _ptr(dqkv), B, T, H, D,
           p_drop, seed, _stream())
 
 
 def xent_fwd(logits, ld, labels, loss_rows, lse, dlogits, ldd, M, V, loss, inv_count, ignore_index=-100):
-    _call("gpt2mi_xent_fwd", _ptr(logits), ld, _ptr(labels), _ptr(loss_rows), _ptr(lse), _ptr(dlogits), ldd, M, V,
+    _call("gpt2mi_xent_fwd_f32" if _f32(logits) else "gpt2mi_xent_fwd", _ptr(logits), ld, _ptr(labels), _ptr(loss_rows), _ptr(lse), _ptr(dlogits), ldd, M, V,
           ignore_index, _ptr(loss), _ptr(inv_count), _stream())
 
 

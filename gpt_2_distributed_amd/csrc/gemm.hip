@@ -228,7 +228,7 @@ GPT2MI_EXPORT int gpt2mi_gemm(int layout, int epilogue, int M, int N, int K, con
   P.C = C;
   P.bias = bias;
   P.resid = resid;
-  P.aux = (bf16*)aux;
+  P.aux = aux;
   P.alpha_dev = alpha_dev;
   P.M = M; P.N = N; P.K = K;
   P.lda = lda; P.ldb = ldb; P.ldc = ldc; P.ldaux = ldaux;

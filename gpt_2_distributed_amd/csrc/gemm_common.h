@@ -18,7 +18,7 @@ struct GemmParams {
   void* C;
   const float* bias;
   const float* resid;
-  bf16* aux;  // EPI_GELU: pre-activation out; EPI_GELU_BWD: pre-activation in
+  void* aux;  // EPI_GELU: pre-activation out; EPI_GELU_BWD: pre-activation in (element type = TE)
   const float* alpha_dev;
   int M, N, K, lda, ldb, ldc, ldaux;
   int k_per_split;
@@ -54,7 +54,26 @@ __device__ __forceinline__ void drop4(const GemmParams& P, uint64_t didx, bool k
   keep[3] = drop_keep16(h1, 1, P.thr);
 }
 
-template <int EPI>
+// 4-element vector load/store of the activation element type TE (bf16 under autocast, fp32 in the
+// fp32 / no-autocast mode of the reference).
+template <typename TE>
+__device__ __forceinline__ void store4(TE* p, f32x4 v) {
+  if constexpr (sizeof(TE) == 2) *reinterpret_cast<bf16x4*>(p) = bf16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+  else *reinterpret_cast<f32x4*>(p) = v;
+}
+template <typename TE>
+__device__ __forceinline__ f32x4 load4(const TE* p) {
+  if constexpr (sizeof(TE) == 2) {
+    bf16x4 t = *reinterpret_cast<const bf16x4*>(p);
+    return f32x4{bf2f(t[0]), bf2f(t[1]), bf2f(t[2]), bf2f(t[3])};
+  } else {
+    return *reinterpret_cast<const f32x4*>(p);
+  }
+}
+
+// Apply the fused epilogue to 4 consecutive outputs C[gm][gn..gn+3]; v = alpha*acc (+bias).
+// TE = element type of the bf16-or-fp32 outputs (C of BF16/GELU/GELU_BWD, aux).
+template <int EPI, typename TE = bf16>
 __device__ __forceinline__ void epilogue_store(const GemmParams& P, int gm, int gn, f32x4 v) {
   const size_t cidx = (size_t)gm * P.ldc + gn;
   const uint64_t didx = (uint64_t)gm * P.N + gn;  // dropout element index in the logical [M,N] (even)
@@ -62,8 +81,7 @@ __device__ __forceinline__ void epilogue_store(const GemmParams& P, int gm, int 
   if (EPI == EPI_RESID || EPI == EPI_GELU || EPI == EPI_GELU_BWD)
     if (P.thr) drop4(P, didx, keep);
   if constexpr (EPI == EPI_BF16) {
-    bf16* C = reinterpret_cast<bf16*>(P.C);
-    *reinterpret_cast<bf16x4*>(C + cidx) = bf16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+    store4<TE>(reinterpret_cast<TE*>(P.C) + cidx, v);
   } else if constexpr (EPI == EPI_F32) {
     float* C = reinterpret_cast<float*>(P.C);
     if (P.accumulate) {
@@ -83,28 +101,26 @@ __device__ __forceinline__ void epilogue_store(const GemmParams& P, int gm, int 
     }
     *reinterpret_cast<f32x4*>(C + cidx) = r;
   } else if constexpr (EPI == EPI_GELU) {
-    bf16* C = reinterpret_cast<bf16*>(P.C);
-    bf16x4 u, h;
+    f32x4 h;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      u[j] = f2bf(v[j]);
       float a = gelu_f(v[j]);
       if (P.thr) a = keep[j] ? a * P.inv_keep : 0.f;
-      h[j] = f2bf(a);
+      h[j] = a;
     }
-    *reinterpret_cast<bf16x4*>(P.aux + (size_t)gm * P.ldaux + gn) = u;
-    *reinterpret_cast<bf16x4*>(C + cidx) = h;
+    store4<TE>(reinterpret_cast<TE*>(P.aux) + (size_t)gm * P.ldaux + gn, v);
+    store4<TE>(reinterpret_cast<TE*>(P.C) + cidx, h);
   } else if constexpr (EPI == EPI_GELU_BWD) {
-    bf16* C = reinterpret_cast<bf16*>(P.C);
-    bf16x4 u = *reinterpret_cast<const bf16x4*>(P.aux + (size_t)gm * P.ldaux + gn);
-    bf16x4 o;
+    // gelu' is evaluated at the STORED pre-activation (bf16-rounded under autocast), as autograd does
+    const f32x4 u = load4<TE>(reinterpret_cast<const TE*>(P.aux) + (size_t)gm * P.ldaux + gn);
+    f32x4 o;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       float d = v[j];
       if (P.thr) d = keep[j] ? d * P.inv_keep : 0.f;
-      o[j] = f2bf(d * gelu_grad_f(bf2f(u[j])));
+      o[j] = d * gelu_grad_f(u[j]);
     }
-    *reinterpret_cast<bf16x4*>(C + cidx) = o;
+    store4<TE>(reinterpret_cast<TE*>(P.C) + cidx, o);
   } else if constexpr (EPI == EPI_ATOMIC) {
     float* C = reinterpret_cast<float*>(P.C);
 #pragma unroll

@@ -54,6 +54,23 @@ __device__ __forceinline__ void load_bf(const bf16* p, float* d) {
   }
 }
 
+template <int VEC, typename T>
+__device__ __forceinline__ void load_t(const T* p, float* d) {
+  if constexpr (sizeof(T) == 2) load_bf<VEC>(p, d);
+  else load_vec<VEC>(p, d);
+}
+template <int VEC, typename T>
+__device__ __forceinline__ void store_t(T* p, const float* d) {
+  if constexpr (sizeof(T) == 2) store_bf<VEC>(p, d);
+  else store_vec<VEC>(p, d);
+}
+// value as stored in T (bf16 rounding), for column sums of what the next GEMM actually reads
+template <typename T>
+__device__ __forceinline__ float as_stored(float v) {
+  if constexpr (sizeof(T) == 2) return bf2f(f2bf(v));
+  else return v;
+}
+
 // ---------------------------------------------------------------------------------------------
 // LayerNorm forward: y = (x-mu)*rstd*w + b, biased variance (nn.LayerNorm). x fp32 [M,C];
 // y bf16 (what autocast feeds the next linear) and/or fp32; mean/rstd fp32 [M] for backward.
@@ -113,11 +130,11 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
 // and, for the NEXT backward GEMM of the residual branch below this LN, emits
 //   out_bf[m] = bf16(dres_new[m] * keep/(1-p))  and  dbias_out += colsum(out_bf)
 // (the branch's dropout mask regenerated from (seed,row*C+c); dbias_out = that branch's bias grad).
-template <int VEC, int NV>
+template <int VEC, int NV, typename TG>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(
     const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ mean,
-    const float* __restrict__ rstd, const bf16* __restrict__ dy, float* __restrict__ dres,
-    float* __restrict__ dw, float* __restrict__ db, bf16* __restrict__ out_bf, float* __restrict__ dbias_out,
+    const float* __restrict__ rstd, const TG* __restrict__ dy, float* __restrict__ dres,
+    float* __restrict__ dw, float* __restrict__ db, TG* __restrict__ out_bf, float* __restrict__ dbias_out,
     int M, int C, int nv, uint64_t seed, uint32_t thr, float inv_keep, int dres_init) {
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
@@ -130,7 +147,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
   for (int row = row0; row < M; row += stride) {
     const float mu = mean[row], rs = rstd[row];
     const float* xr = x + (size_t)row * C;
-    const bf16* gr = dy + (size_t)row * C;
+    const TG* gr = dy + (size_t)row * C;
     float xh[NV * VEC], g[NV * VEC];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -139,7 +156,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
         const int e = VEC * (lane + 64 * i);
         float wv[VEC];
         load_vec<VEC>(xr + e, xh + VEC * i);
-        load_bf<VEC>(gr + e, g + VEC * i);
+        load_t<VEC, TG>(gr + e, g + VEC * i);
         load_vec<VEC>(w + e, wv);
 #pragma unroll
         for (int j = 0; j < VEC; ++j) {
@@ -181,10 +198,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
             if (thr) val = drop_keep(seed, (uint64_t)row * C + e + j, thr) ? val * inv_keep : 0.f;
             o[j] = val;
           }
-          store_bf<VEC>(out_bf + (size_t)row * C + e, o);
+          store_t<VEC, TG>(out_bf + (size_t)row * C + e, o);
           if (dbias_out) {
 #pragma unroll
-            for (int j = 0; j < VEC; ++j) abo[VEC * i + j] += bf2f(f2bf(o[j]));
+            for (int j = 0; j < VEC; ++j) abo[VEC * i + j] += as_stored<TG>(o[j]);
           }
         }
       }
@@ -276,7 +293,8 @@ __global__ __launch_bounds__(256) void embed_bwd_wpe_kernel(const float* __restr
 
 // Column sums of a bf16 [M,N] matrix with row stride ld: db[n] += sum_m g[m,n]. Each thread owns
 // 4 adjacent columns (8-B loads); blockIdx.y splits rows; one atomic per column per block-row-chunk.
-__global__ __launch_bounds__(256) void colsum_bf16_kernel(const bf16* __restrict__ g, float* __restrict__ db, int M,
+template <typename TG>
+__global__ __launch_bounds__(256) void colsum_kernel(const TG* __restrict__ g, float* __restrict__ db, int M,
                                                           int N, int ld, int rows_per_block) {
   const int col4 = (blockIdx.x * 64 + (threadIdx.x & 63)) * 4;
   const int sub = threadIdx.x >> 6;  // 4 row groups per block
@@ -285,9 +303,10 @@ __global__ __launch_bounds__(256) void colsum_bf16_kernel(const bf16* __restrict
   float s[4] = {0.f, 0.f, 0.f, 0.f};
   if (col4 < N) {
     for (int r = r0 + sub; r < r1; r += 4) {
-      bf16x4 v = *reinterpret_cast<const bf16x4*>(g + (size_t)r * ld + col4);
+      float v[4];
+      load_t<4, TG>(g + (size_t)r * ld + col4, v);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) s[j] += bf2f(v[j]);
+      for (int j = 0; j < 4; ++j) s[j] += v[j];
     }
   }
   __shared__ float red[4][256];
@@ -336,10 +355,10 @@ GPT2MI_EXPORT int gpt2mi_layernorm_fwd(const float* x, const float* w, const flo
   return gpt2mi::check_launch("layernorm_fwd");
 }
 
-GPT2MI_EXPORT int gpt2mi_layernorm_bwd(const float* x, const float* w, const float* mean, const float* rstd,
-                                       const uint16_t* dy, float* dres, float* dw, float* db, uint16_t* out_bf16,
-                                       float* dbias_out, int M, int C, float p_out, uint64_t seed_out, int dres_init,
-                                       void* stream) {
+template <typename TG>
+static int layernorm_bwd_t(const float* x, const float* w, const float* mean, const float* rstd, const TG* dy,
+                           float* dres, float* dw, float* db, TG* out, float* dbias_out, int M, int C, float p_out,
+                           uint64_t seed_out, int dres_init, void* stream) {
   int vec, nv;
   GPT2MI_REQUIRE(row_shape(C, &vec, &nv), "layernorm_bwd: unsupported C=%d", C);
   hipStream_t s = (hipStream_t)stream;
@@ -347,10 +366,26 @@ GPT2MI_EXPORT int gpt2mi_layernorm_bwd(const float* x, const float* w, const flo
   const size_t sh = (size_t)kWaves * C * sizeof(float);
   const uint32_t thr = drop_threshold(p_out);
   const float ik = p_out > 0.f ? 1.f / (1.f - p_out) : 1.f;
-#define X(V, N) if (vec == V && nv == N) ln_bwd_kernel<V, N><<<g, 256, sh, s>>>(x, w, mean, rstd, (const bf16*)dy, dres, dw, db, (bf16*)out_bf16, dbias_out, M, C, nv, seed_out, thr, ik, dres_init);
+#define X(V, N) if (vec == V && nv == N) ln_bwd_kernel<V, N, TG><<<g, 256, sh, s>>>(x, w, mean, rstd, dy, dres, dw, db, out, dbias_out, M, C, nv, seed_out, thr, ik, dres_init);
   GPT2MI_ROW_CASES(X)
 #undef X
   return gpt2mi::check_launch("layernorm_bwd");
+}
+
+GPT2MI_EXPORT int gpt2mi_layernorm_bwd(const float* x, const float* w, const float* mean, const float* rstd,
+                                       const uint16_t* dy, float* dres, float* dw, float* db, uint16_t* out_bf16,
+                                       float* dbias_out, int M, int C, float p_out, uint64_t seed_out, int dres_init,
+                                       void* stream) {
+  return layernorm_bwd_t<bf16>(x, w, mean, rstd, (const bf16*)dy, dres, dw, db, (bf16*)out_bf16, dbias_out, M, C,
+                               p_out, seed_out, dres_init, stream);
+}
+
+GPT2MI_EXPORT int gpt2mi_layernorm_bwd_f32(const float* x, const float* w, const float* mean, const float* rstd,
+                                           const float* dy, float* dres, float* dw, float* db, float* out_f32,
+                                           float* dbias_out, int M, int C, float p_out, uint64_t seed_out,
+                                           int dres_init, void* stream) {
+  return layernorm_bwd_t<float>(x, w, mean, rstd, dy, dres, dw, db, out_f32, dbias_out, M, C, p_out, seed_out,
+                                dres_init, stream);
 }
 
 GPT2MI_EXPORT int gpt2mi_embed_fwd(const int64_t* idx, const float* wte, const float* wpe, float* x, int B, int T,
@@ -380,11 +415,20 @@ GPT2MI_EXPORT int gpt2mi_embed_bwd(const int64_t* idx, const float* dres, float*
   return gpt2mi::check_launch("embed_bwd_wpe");
 }
 
-GPT2MI_EXPORT int gpt2mi_colsum_bf16(const uint16_t* g, float* db, int M, int N, int ld, void* stream) {
-  GPT2MI_REQUIRE(N % 4 == 0 && ld % 4 == 0, "colsum_bf16: N=%d and ld=%d must be multiples of 4", N, ld);
+template <typename TG>
+static int colsum_t(const TG* g, float* db, int M, int N, int ld, void* stream) {
+  GPT2MI_REQUIRE(N % 4 == 0 && ld % 4 == 0, "colsum: N=%d and ld=%d must be multiples of 4", N, ld);
   hipStream_t s = (hipStream_t)stream;
   const int rpb = 256;
   dim3 grid((N + 255) / 256, (M + rpb - 1) / rpb);
-  colsum_bf16_kernel<<<grid, 256, 0, s>>>((const bf16*)g, db, M, N, ld, rpb);
-  return gpt2mi::check_launch("colsum_bf16");
+  colsum_kernel<TG><<<grid, 256, 0, s>>>(g, db, M, N, ld, rpb);
+  return gpt2mi::check_launch("colsum");
+}
+
+GPT2MI_EXPORT int gpt2mi_colsum_bf16(const uint16_t* g, float* db, int M, int N, int ld, void* stream) {
+  return colsum_t<bf16>((const bf16*)g, db, M, N, ld, stream);
+}
+
+GPT2MI_EXPORT int gpt2mi_colsum_f32(const float* g, float* db, int M, int N, int ld, void* stream) {
+  return colsum_t<float>(g, db, M, N, ld, stream);
 }

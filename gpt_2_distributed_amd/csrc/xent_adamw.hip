@@ -13,21 +13,50 @@ namespace {
 //   loss_row = lse - logit[label]  (0 and not counted when label == ignore_index)
 //   pass 2: dlogits = softmax - onehot (bf16, unscaled; the 1/N and upstream grad are applied as
 //           the alpha of the backward GEMMs), zero in the padded columns [V, ld_d).
-__global__ __launch_bounds__(256) void xent_fwd_kernel(const bf16* __restrict__ logits, int ld,
+template <typename TL>
+__device__ __forceinline__ void load8(const TL* p, float* f) {
+  if constexpr (sizeof(TL) == 2) {
+    bf16x8 v = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = bf2f(v[j]);
+  } else {
+    const f32x4 a = reinterpret_cast<const f32x4*>(p)[0], b = reinterpret_cast<const f32x4*>(p)[1];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      f[j] = a[j];
+      f[4 + j] = b[j];
+    }
+  }
+}
+template <typename TL>
+__device__ __forceinline__ void store8(TL* p, const float* f) {
+  if constexpr (sizeof(TL) == 2) {
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(f[j]);
+    *reinterpret_cast<bf16x8*>(p) = o;
+  } else {
+    reinterpret_cast<f32x4*>(p)[0] = f32x4{f[0], f[1], f[2], f[3]};
+    reinterpret_cast<f32x4*>(p)[1] = f32x4{f[4], f[5], f[6], f[7]};
+  }
+}
+
+template <typename TL>
+__global__ __launch_bounds__(256) void xent_fwd_kernel(const TL* __restrict__ logits, int ld,
                                                        const int64_t* __restrict__ labels, float* __restrict__ loss_rows,
-                                                       float* __restrict__ lse_out, bf16* __restrict__ dlogits, int ldd,
+                                                       float* __restrict__ lse_out, TL* __restrict__ dlogits, int ldd,
                                                        int V, int ignore_index) {
   const int row = blockIdx.x;
-  const bf16* lp = logits + (size_t)row * ld;
+  const TL* lp = logits + (size_t)row * ld;
   const int tid = threadIdx.x;
   float m = -INFINITY, s = 0.f;
   for (int c = 8 * tid; c < V; c += 8 * 256) {
-    bf16x8 v = *reinterpret_cast<const bf16x8*>(lp + c);
     float f[8];
+    load8<TL>(lp + c, f);
     float cm = -INFINITY;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      f[j] = (c + j < V) ? bf2f(v[j]) : -INFINITY;
+      f[j] = (c + j < V) ? f[j] : -INFINITY;
       cm = fmaxf(cm, f[j]);
     }
     const float nm = fmaxf(m, cm);
@@ -61,28 +90,27 @@ __global__ __launch_bounds__(256) void xent_fwd_kernel(const bf16* __restrict__ 
     s_lse = lse;
     lse_out[row] = lse;
     const int64_t y = labels[row];
-    loss_rows[row] = (y == ignore_index) ? 0.f : lse - bf2f(lp[y]);
+    loss_rows[row] = (y == ignore_index) ? 0.f : lse - (float)lp[y];
   }
   __syncthreads();
   if (!dlogits) return;
   const float lse = s_lse;
   const int64_t y = labels[row];
-  bf16* dp = dlogits + (size_t)row * ldd;
+  TL* dp = dlogits + (size_t)row * ldd;
   const bool ign = (y == ignore_index);
   for (int c = 8 * tid; c < ldd; c += 8 * 256) {
-    bf16x8 o;
+    float o[8];
     if (c < V) {
-      bf16x8 v = *reinterpret_cast<const bf16x8*>(lp + c);
+      float v[8];
+      load8<TL>(lp + c, v);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float d = (c + j < V && !ign) ? __expf(bf2f(v[j]) - lse) - ((c + j == y) ? 1.f : 0.f) : 0.f;
-        o[j] = f2bf(d);
-      }
+      for (int j = 0; j < 8; ++j)
+        o[j] = (c + j < V && !ign) ? __expf(v[j] - lse) - ((c + j == y) ? 1.f : 0.f) : 0.f;
     } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = f2bf(0.f);
+      for (int j = 0; j < 8; ++j) o[j] = 0.f;
     }
-    *reinterpret_cast<bf16x8*>(dp + c) = o;
+    store8<TL>(dp + c, o);
   }
 }
 
@@ -196,18 +224,31 @@ constexpr int kNormBlocks = 2048;
 
 }  // namespace
 
-GPT2MI_EXPORT int gpt2mi_xent_fwd(const uint16_t* logits, int ld, const int64_t* labels, float* loss_rows, float* lse,
-                                  uint16_t* dlogits, int ldd, int M, int V, int ignore_index, float* loss,
-                                  float* inv_count, void* stream) {
+template <typename TL>
+static int xent_fwd_t(const TL* logits, int ld, const int64_t* labels, float* loss_rows, float* lse, TL* dlogits,
+                      int ldd, int M, int V, int ignore_index, float* loss, float* inv_count, void* stream) {
   GPT2MI_REQUIRE(ld % 8 == 0 && ld >= V && (dlogits == nullptr || (ldd % 8 == 0 && ldd >= V)),
                  "xent_fwd: row strides must be multiples of 8 and >= V (ld=%d ldd=%d V=%d)", ld, ldd, V);
   hipStream_t s = (hipStream_t)stream;
-  xent_fwd_kernel<<<M, 256, 0, s>>>((const bf16*)logits, ld, labels, loss_rows, lse, (bf16*)dlogits, ldd, V,
-                                    ignore_index);
+  xent_fwd_kernel<TL><<<M, 256, 0, s>>>(logits, ld, labels, loss_rows, lse, dlogits, ldd, V, ignore_index);
   int rc = gpt2mi::check_launch("xent_fwd");
   if (rc) return rc;
   xent_finalize_kernel<<<1, 1024, 0, s>>>(loss_rows, labels, M, ignore_index, loss, inv_count);
   return gpt2mi::check_launch("xent_finalize");
+}
+
+GPT2MI_EXPORT int gpt2mi_xent_fwd(const uint16_t* logits, int ld, const int64_t* labels, float* loss_rows, float* lse,
+                                  uint16_t* dlogits, int ldd, int M, int V, int ignore_index, float* loss,
+                                  float* inv_count, void* stream) {
+  return xent_fwd_t<bf16>((const bf16*)logits, ld, labels, loss_rows, lse, (bf16*)dlogits, ldd, M, V, ignore_index,
+                          loss, inv_count, stream);
+}
+
+GPT2MI_EXPORT int gpt2mi_xent_fwd_f32(const float* logits, int ld, const int64_t* labels, float* loss_rows, float* lse,
+                                      float* dlogits, int ldd, int M, int V, int ignore_index, float* loss,
+                                      float* inv_count, void* stream) {
+  return xent_fwd_t<float>(logits, ld, labels, loss_rows, lse, dlogits, ldd, M, V, ignore_index, loss, inv_count,
+                           stream);
 }
 
 GPT2MI_EXPORT int gpt2mi_adamw(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, size_t n, float lr,

@@ -58,10 +58,11 @@ class BlockActs:
 
 
 class Workspace:
-    def __init__(self, cfg, B: int, T: int, vpad: int, device):
+    def __init__(self, cfg, B: int, T: int, vpad: int, device, act=BF16):
         L, C, H = cfg.n_layer, cfg.n_embd, cfg.n_head
         M = B * T
-        e = lambda *s, dt=BF16: torch.empty(*s, dtype=dt, device=device)  # noqa: E731
+        e = lambda *s, dt=act: torch.empty(*s, dtype=dt, device=device)  # noqa: E731
+        self.act = act
         self.B, self.T, self.M = B, T, M
         self.x = e(L + 1, M, C, dt=F32)
         self.blocks: List[BlockActs] = []
@@ -89,7 +90,7 @@ class Workspace:
         # split-K slabs of the 256x256 wgrad GEMMs
         wshapes = [(3 * C, C), (C, C), (4 * C, C), (C, 4 * C), (vpad, C)]
         need = max((K_wgrad_splits(m, n, M) * m * n if K_wgrad_splits(m, n, M) > 1 else 0)
-                   for m, n in wshapes) if C % 256 == 0 else 0
+                   for m, n in wshapes) if C % 256 == 0 and act == BF16 else 0
         self.wgrad_ws = e(max(need, 4), dt=F32)
 
 
@@ -234,13 +235,40 @@ class Engine:
                 raise RuntimeError(f"{n}.grad is not a view of the engine's grad arena; zero grads with "
                                    "set_to_none=True or the model's optimizer before backward")
 
-    def workspace(self, B, T) -> Workspace:
-        key = (B, T)
+    def workspace(self, B, T, act=BF16) -> Workspace:
+        key = (B, T, act)
         if key not in self._ws:
             self._ws.clear()  # one live shape at a time keeps HBM use bounded
             torch.cuda.empty_cache()
-            self._ws[key] = Workspace(self.cfg, B, T, self.vpad, self.device)
+            self._ws[key] = Workspace(self.cfg, B, T, self.vpad, self.device, act)
         return self._ws[key]
+
+    # ---- precision ----------------------------------------------------------------------------------
+    def compute_dtype(self) -> torch.dtype:
+        """bf16 under ``torch.autocast("cuda", torch.bfloat16)`` (the reference trainer,
+        train_gpt2_distributed.py:404), fp32 without autocast (the reference model.py run plain), unless
+        ``model.precision`` forces "bf16" / "fp32"."""
+        p = getattr(self.model, "precision", "auto")
+        if p == "bf16":
+            return BF16
+        if p == "fp32":
+            return F32
+        if p != "auto":
+            raise ValueError(f"GPT2.precision must be 'auto', 'bf16' or 'fp32' (got {p!r})")
+        if torch.is_autocast_enabled("cuda"):
+            dt = torch.get_autocast_dtype("cuda")
+            if dt != BF16:
+                raise NotImplementedError(f"autocast dtype {dt}: the MI355X kernels implement bf16 autocast only")
+            return BF16
+        return F32
+
+    def w(self, name, act):
+        """GEMM operand of a weight: the bf16 shadow under autocast, the fp32 master weight otherwise
+        (wte as its zero-padded [Vp, C] slot for the tied lm_head)."""
+        if act == BF16:
+            return self.w16(name)
+        s = self.layout.slots[name]
+        return self.model.arena[s.offset:s.offset + s.reserved]
 
     # ---- public entry -------------------------------------------------------------------------------
     def forward(self, idx: torch.Tensor, labels: Optional[torch.Tensor]):
@@ -277,13 +305,16 @@ class Engine:
         idx = idx.contiguous()
         if labels is not None:
             labels = labels.contiguous().long()
-        self._maybe_refresh_shadow()
-        ws = self.workspace(B, T)
+        act = self.compute_dtype()
+        if act == BF16:
+            self._maybe_refresh_shadow()
+        ws = self.workspace(B, T, act)
+        W = lambda n: self.w(n, act)  # noqa: E731
         pr, pa = self._dropout()
         self._step_seed += 1
         seeds = self._seeds(self._step_seed)
         self._fwd_token += 1
-        self._saved = (idx, labels, pr, pa, seeds)
+        self._saved = (idx, labels, pr, pa, seeds, act)
 
         x = ws.x
         K.embed_fwd(idx, self.p("transformer.wte.weight"), self.p("transformer.wpe.weight"), x[0], B, T, C, pr,
@@ -293,23 +324,23 @@ class Engine:
             pre = f"transformer.h.{l}."
             K.layernorm_fwd(x[l], self.p(pre + "ln1.weight"), self.p(pre + "ln1.bias"), A.ln1, None, A.m1, A.r1,
                             M, C, cfg.layer_norm_eps)
-            K.gemm(K.FWD, K.EPI_BF16, M, 3 * C, C, A.ln1, C, self.w16(pre + "attn.qkv.weight"), C, A.qkv, 3 * C,
+            K.gemm(K.FWD, K.EPI_BF16, M, 3 * C, C, A.ln1, C, W(pre + "attn.qkv.weight"), C, A.qkv, 3 * C,
                    bias=self.p(pre + "attn.qkv.bias"))
             with self._probe("attn_fwd"):
                 K.attn_fwd(A.qkv, A.ao, A.lse, B, T, H, C // H, pa, seeds[("attn", l)])
-            K.gemm(K.FWD, K.EPI_RESID, M, C, C, A.ao, C, self.w16(pre + "attn.proj.weight"), C, A.xmid, C,
+            K.gemm(K.FWD, K.EPI_RESID, M, C, C, A.ao, C, W(pre + "attn.proj.weight"), C, A.xmid, C,
                    bias=self.p(pre + "attn.proj.bias"), resid=x[l], p_drop=pr, seed=seeds[("proj", l)])
             K.layernorm_fwd(A.xmid, self.p(pre + "ln2.weight"), self.p(pre + "ln2.bias"), A.ln2, None, A.m2, A.r2,
                             M, C, cfg.layer_norm_eps)
             with self._probe("fc1_fwd"):
-                K.gemm(K.FWD, K.EPI_GELU, M, 4 * C, C, A.ln2, C, self.w16(pre + "mlp.fc1.weight"), C, A.h, 4 * C,
+                K.gemm(K.FWD, K.EPI_GELU, M, 4 * C, C, A.ln2, C, W(pre + "mlp.fc1.weight"), C, A.h, 4 * C,
                        bias=self.p(pre + "mlp.fc1.bias"), aux=A.u, ldaux=4 * C, p_drop=pr, seed=seeds[("fc1", l)])
-            K.gemm(K.FWD, K.EPI_RESID, M, C, 4 * C, A.h, 4 * C, self.w16(pre + "mlp.fc2.weight"), 4 * C, x[l + 1], C,
+            K.gemm(K.FWD, K.EPI_RESID, M, C, 4 * C, A.h, 4 * C, W(pre + "mlp.fc2.weight"), 4 * C, x[l + 1], C,
                    bias=self.p(pre + "mlp.fc2.bias"), resid=A.xmid, p_drop=pr, seed=seeds[("fc2", l)])
         K.layernorm_fwd(x[L], self.p("transformer.ln_f.weight"), self.p("transformer.ln_f.bias"), ws.lnf, None,
                         ws.mf, ws.rf, M, C, cfg.layer_norm_eps)
         with self._probe("lm_head_fwd"):
-            K.gemm(K.FWD, K.EPI_BF16, M, Vp, C, ws.lnf, C, self.w16("transformer.wte.weight"), C, ws.logits, Vp)
+            K.gemm(K.FWD, K.EPI_BF16, M, Vp, C, ws.lnf, C, W("transformer.wte.weight"), C, ws.logits, Vp)
         loss = None
         if labels is not None:
             loss = torch.empty((), dtype=F32, device=self.device)  # fresh: callers may keep it across steps
@@ -321,12 +352,13 @@ class Engine:
     # ---- backward -----------------------------------------------------------------------------------
     def _backward(self, grad_loss: torch.Tensor):
         cfg = self.cfg
-        idx, labels, pr, pa, seeds = self._saved
+        idx, labels, pr, pa, seeds, act = self._saved
         B, T = idx.shape
         C, H, L = cfg.n_embd, cfg.n_head, cfg.n_layer
         Vp = self.vpad
         M = B * T
-        ws = self.workspace(B, T)
+        ws = self.workspace(B, T, act)
+        W = lambda n: self.w(n, act)  # noqa: E731
         self._prepare_grads()
         if grad_loss is None:
             return
@@ -339,7 +371,9 @@ class Engine:
 
         def wgrad(m, n, a, lda, b, ldb, out):
             # dW[m][n] += dY[:, :m]^T X[:, :n] over the M tokens
-            if m % 256 == 0 and n % 256 == 0:
+            if act == F32:
+                K.gemm(K.WGRAD, K.EPI_F32, m, n, M, a, lda, b, ldb, out, n, accumulate=True)
+            elif m % 256 == 0 and n % 256 == 0:
                 K.gemm_wgrad(m, n, M, a, lda, b, ldb, out, n, accumulate=True, workspace=ws.wgrad_ws,
                              splits=K_wgrad_splits(m, n, M))
             else:
@@ -348,11 +382,11 @@ class Engine:
 
         # lm_head (tied): dlnf = dlogits @ wte ; dwte (+)= dlogits^T @ lnf
         with self._probe("lm_head_dgrad"):
-            K.gemm(K.DGRAD, K.EPI_BF16, M, C, Vp, ws.dlogits, Vp, self.w16("transformer.wte.weight"), C, ws.dln, C,
+            K.gemm(K.DGRAD, K.EPI_BF16, M, C, Vp, ws.dlogits, Vp, W("transformer.wte.weight"), C, ws.dln, C,
                    alpha_dev=ws.dscale)
         wte_g = self.layout.padded_view(self.grad, "transformer.wte.weight", Vp)
         with self._probe("lm_head_wgrad"):
-            if C % 256 == 0:
+            if C % 256 == 0 and act == BF16:
                 K.gemm_wgrad(Vp, C, M, ws.dlogits, Vp, ws.lnf, C, wte_g, C, accumulate=True, alpha_dev=ws.dscale,
                              workspace=ws.wgrad_ws, splits=K_wgrad_splits(Vp, C, M))
             else:
@@ -368,20 +402,20 @@ class Engine:
             A = ws.blocks[l]
             pre = f"transformer.h.{l}."
             # ---- MLP: dY2 = dres_bf (fc2 dropout applied), db2 done by the LN bwd above
-            K.gemm(K.DGRAD, K.EPI_GELU_BWD, M, 4 * C, C, ws.dres_bf, C, self.w16(pre + "mlp.fc2.weight"), 4 * C,
+            K.gemm(K.DGRAD, K.EPI_GELU_BWD, M, 4 * C, C, ws.dres_bf, C, W(pre + "mlp.fc2.weight"), 4 * C,
                    ws.dU, 4 * C, aux=A.u, ldaux=4 * C, p_drop=pr, seed=seeds[("fc1", l)])
             wgrad(C, 4 * C, ws.dres_bf, C, A.h, 4 * C, self.g(pre + "mlp.fc2.weight"))
-            K.gemm(K.DGRAD, K.EPI_BF16, M, C, 4 * C, ws.dU, 4 * C, self.w16(pre + "mlp.fc1.weight"), C, ws.dln, C)
+            K.gemm(K.DGRAD, K.EPI_BF16, M, C, 4 * C, ws.dU, 4 * C, W(pre + "mlp.fc1.weight"), C, ws.dln, C)
             wgrad(4 * C, C, ws.dU, 4 * C, A.ln2, C, self.g(pre + "mlp.fc1.weight"))
             K.colsum_bf16(ws.dU, self.g(pre + "mlp.fc1.bias"), M, 4 * C, 4 * C)
             K.layernorm_bwd(A.xmid, self.p(pre + "ln2.weight"), A.m2, A.r2, ws.dln, ws.dres, self.g(pre + "ln2.weight"),
                             self.g(pre + "ln2.bias"), ws.dres_bf, self.g(pre + "attn.proj.bias"), M, C, pr,
                             seeds[("proj", l)])
             # ---- attention
-            K.gemm(K.DGRAD, K.EPI_BF16, M, C, C, ws.dres_bf, C, self.w16(pre + "attn.proj.weight"), C, ws.dln, C)
+            K.gemm(K.DGRAD, K.EPI_BF16, M, C, C, ws.dres_bf, C, W(pre + "attn.proj.weight"), C, ws.dln, C)
             wgrad(C, C, ws.dres_bf, C, A.ao, C, self.g(pre + "attn.proj.weight"))
             K.attn_bwd(A.qkv, A.ao, ws.dln, A.lse, ws.delta, ws.dqkv, B, T, H, C // H, pa, seeds[("attn", l)])
-            K.gemm(K.DGRAD, K.EPI_BF16, M, C, 3 * C, ws.dqkv, 3 * C, self.w16(pre + "attn.qkv.weight"), C, ws.dln, C)
+            K.gemm(K.DGRAD, K.EPI_BF16, M, C, 3 * C, ws.dqkv, 3 * C, W(pre + "attn.qkv.weight"), C, ws.dln, C)
             wgrad(3 * C, C, ws.dqkv, 3 * C, A.ln1, C, self.g(pre + "attn.qkv.weight"))
             K.colsum_bf16(ws.dqkv, self.g(pre + "attn.qkv.bias"), M, 3 * C, 3 * C)
             if l > 0:

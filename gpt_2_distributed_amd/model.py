@@ -13,8 +13,11 @@ What differs underneath (MI355X-first):
   single passes; ``wte`` is padded to a multiple of 256 rows for the lm_head tiling;
 * ``GPT2.forward`` is ONE autograd node: forward and backward of the whole network are explicit
   sequences of HIP kernels (``engine.py``) with bf16 MFMA GEMMs, fused epilogues, flash attention;
-  it always computes with the CUDA-autocast-bf16 numerics of the reference trainer
-  (train_gpt2_distributed.py:404), with or without an enclosing ``torch.autocast``;
+  under ``torch.autocast("cuda", torch.bfloat16)`` (the reference trainer,
+  train_gpt2_distributed.py:404) it computes with CUDA-autocast-bf16 numerics (bf16 MFMA operands,
+  fp32 LayerNorm/softmax/loss/residual); without autocast it computes in fp32 like the plain
+  reference module (fp32 MFMA GEMMs, fp32 attention). ``model.precision = "bf16" | "fp32"``
+  overrides the autocast-following default ``"auto"``;
 * no [T,T] ``mask`` buffer (model.py:105-108): causality comes from tile indices (the buffer was
   non-persistent, so state_dicts are unchanged).
 The GPU path has no CPU fallback: a CPU ``forward`` raises.
@@ -147,6 +150,7 @@ class GPT2(nn.Module):
         self.lm_head.weight = self.transformer.wte.weight
         self._pack_arena()
         self._engine = None
+        self.precision = "auto"  # "auto": follow torch.autocast("cuda"); or force "bf16" / "fp32"
 
     # ---- flat arena ------------------------------------------------------------------------------
     def _pack_arena(self):

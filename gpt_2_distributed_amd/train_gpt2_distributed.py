@@ -165,8 +165,9 @@ def main(argv=None):
             last = (accum + 1) % args.grad_accum_steps == 0
             ctx = model.no_sync() if (hasattr(model, "no_sync") and not last) else _Null()
             with ctx:
-                _, loss = model(x, labels=y)
-                loss = loss / args.grad_accum_steps
+                with torch.autocast("cuda", dtype=torch.bfloat16):  # as train_gpt2_distributed.py:404
+                    _, loss = model(x, labels=y)
+                    loss = loss / args.grad_accum_steps
                 loss.backward()
             accum += 1
             if not last:

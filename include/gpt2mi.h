@@ -95,6 +95,29 @@ int gpt2mi_adamw(float* p, const float* g, float* m, float* v, uint16_t* p_bf16,
 int gpt2mi_grad_norm(const float* g, size_t n, float scale, float* partials, float* out, void* stream);
 int gpt2mi_norm_partials_size(void);
 
+/* ---- fp32 mode: the reference model.py run WITHOUT torch.autocast (plain fp32 module; the CPU
+ * trajectory goldens and the north star's "fp32 loss within 1e-4" gate). Same contracts as the bf16
+ * entries above with every activation / weight operand fp32 (C and aux of the "BF16", GELU and
+ * GELU_BWD epilogues are fp32 too). GEMM products are exact fp32 (v_mfma_f32_16x16x4_f32). ---- */
+/* K3/K9-K12/K14 in fp32: N % 4 == 0, K % (16*splits) == 0, leading dims % 4 == 0. */
+int gpt2mi_gemm_f32(int layout, int epilogue, int M, int N, int K, const float* A, int lda, const float* B, int ldb,
+                    void* C, int ldc, const float* bias, const float* resid, float* aux, int ldaux, float alpha,
+                    const float* alpha_dev, int accumulate, int splits, float p_drop, uint64_t seed, void* stream);
+/* K4-K8 in fp32 (model.py:124-155 without autocast); same dropout mask as gpt2mi_attn_fwd. */
+int gpt2mi_attn_fwd_f32(const float* qkv, float* out, float* lse, int B, int T, int H, int head_dim, float p_drop,
+                        uint64_t seed, void* stream);
+int gpt2mi_attn_bwd_f32(const float* qkv, const float* out, const float* dout, const float* lse, float* delta,
+                        float* dqkv, int B, int T, int H, int head_dim, float p_drop, uint64_t seed, void* stream);
+/* LayerNorm backward with fp32 dy and fp32 branch output (see gpt2mi_layernorm_bwd). */
+int gpt2mi_layernorm_bwd_f32(const float* x, const float* w, const float* mean, const float* rstd, const float* dy,
+                             float* dres, float* dw, float* db, float* out_f32, float* dbias_out, int M, int C,
+                             float p_out, uint64_t seed_out, int dres_init, void* stream);
+int gpt2mi_colsum_f32(const float* g, float* db, int M, int N, int ld, void* stream);
+/* K13 on fp32 logits (the fp32 lm_head output), fp32 dlogits. */
+int gpt2mi_xent_fwd_f32(const float* logits, int ld, const int64_t* labels, float* loss_rows, float* lse,
+                        float* dlogits, int ldd, int M, int V, int ignore_index, float* loss, float* inv_count,
+                        void* stream);
+
 /* GEMM kernel selection for A/B benchmarking: 0 = auto (256x256 tiles for layouts 0/1 when N % 256 == 0),
  * 1 = always the 128x128 kernel. */
 void gpt2mi_set_gemm_impl(int impl);

@@ -7,6 +7,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if REPO not in sys.path:
     sys.path.insert(0, REPO)
 
+REPO = REPO
 GOLDEN = os.path.join(REPO, "tests", "golden")
 
 

@@ -30,7 +30,8 @@ for step in range(3):
     t = toks[step].cuda()
     x, y = t[:, :-1], t[:, 1:]
     xs, ys = x[2 * r:2 * r + 2], y[2 * r:2 * r + 2]   # rank r gets half of the batch
-    _, loss = ddp(xs, labels=ys)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        _, loss = ddp(xs, labels=ys)
     loss.backward()
     opt.step(); opt.zero_grad()
     lt = loss.detach().clone(); dist.all_reduce(lt); losses.append(lt.item() / w)
@@ -63,7 +64,8 @@ def test_ddp_two_ranks_matches_single_process(tmp_path):
     losses = []
     for step in range(3):
         t = toks[step].cuda()
-        _, loss = m(t[:, :-1], labels=t[:, 1:])
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            _, loss = m(t[:, :-1], labels=t[:, 1:])
         loss.backward()
         opt.step()
         opt.zero_grad()

@@ -1,7 +1,10 @@
 """End-to-end parity of the HIP training step against the reference goldens (dropout 0).
 
-Tolerances (north star): bf16 loss within 2e-2 relative of the reference fp32 trajectory; per-op
-grads at bf16 GEMM resolution."""
+Two precisions, as the reference runs: under torch.autocast("cuda", bf16) (its trainer,
+train_gpt2_distributed.py:404) and plain fp32 (model.py without autocast: the golden trajectories
+were made that way on CPU). Tolerances (north star): fp32 loss within 1e-4 relative of the reference
+at every one of 20 steps, bf16 loss within 2e-2; per-op grads at fp32 / bf16 GEMM resolution."""
+import contextlib
 import json
 import os
 import tempfile
@@ -24,6 +27,17 @@ def _gpu():
         pytest.skip("no GPU")
 
 
+def prec_ctx(prec):
+    """bf16 = the reference trainer's autocast region; fp32 = no autocast (plain model.py)."""
+    if prec == "bf16":
+        return torch.autocast("cuda", dtype=torch.bfloat16)
+    return contextlib.nullcontext()
+
+
+# per precision: logits rel err, loss rel err, grad rel err, trajectory loss rel err, grad-norm rel err
+TOL = {"bf16": (1e-2, 2e-3, 3e-2, 2e-2, 5e-2), "fp32": (1e-5, 1e-5, 1e-4, 1e-4, 1e-3)}
+
+
 def rel_err(a, b):
     a, b = a.double(), b.double()
     return float((a - b).norm() / (b.norm() + 1e-30))
@@ -34,23 +48,29 @@ def _tiny_model():
     return GPT2(GPT2Config(**TINY)).to(dev)
 
 
-def test_tiny_forward_backward_vs_reference_golden():
+@pytest.mark.parametrize("prec", ["bf16", "fp32"])
+def test_tiny_forward_backward_vs_reference_golden(prec):
+    t_logits, t_loss, t_grad = TOL[prec][:3]
     g = np.load(os.path.join(GOLDEN, "tiny_fwd_bwd.npz"))
     m = _tiny_model()
     idx = torch.from_numpy(g["idx"]).to(dev)
     labels = torch.from_numpy(g["labels"]).to(dev)
-    logits, loss = m(idx, labels=labels)
-    assert logits.shape == (2, 64, 509) and logits.dtype == torch.bfloat16
-    assert rel_err(logits.float().cpu(), torch.from_numpy(g["logits"])) < 1e-2
-    assert abs(loss.item() - float(g["loss"])) / float(g["loss"]) < 2e-3
+    with prec_ctx(prec):
+        logits, loss = m(idx, labels=labels)
+    assert logits.shape == (2, 64, 509)
+    assert logits.dtype == (torch.bfloat16 if prec == "bf16" else torch.float32)
+    assert rel_err(logits.float().cpu(), torch.from_numpy(g["logits"])) < t_logits
+    assert abs(loss.item() - float(g["loss"])) / float(g["loss"]) < t_loss
     loss.backward()
     for n, p in m.named_parameters():
         ref = torch.from_numpy(g["grad:" + n])
         e = rel_err(p.grad.cpu(), ref)
-        assert e < 3e-2, (n, e)
+        assert e < t_grad, (n, e)
 
 
-def test_tiny_trajectory_vs_reference_golden():
+@pytest.mark.parametrize("prec", ["bf16", "fp32"])
+def test_tiny_trajectory_vs_reference_golden(prec):
+    t_loss, t_norm = TOL[prec][3:]
     ref = json.load(open(os.path.join(GOLDEN, "tiny_traj.json")))
     m = _tiny_model()
     opt = m.configure_optimizers(weight_decay=0.1, learning_rate=1e-4, betas=(0.9, 0.95))
@@ -60,16 +80,17 @@ def test_tiny_trajectory_vs_reference_golden():
     for t in toks:
         x = torch.from_numpy(t[:, :-1].copy()).to(dev)
         y = torch.from_numpy(t[:, 1:].copy()).to(dev)
-        _, loss = m(x, labels=y)
+        with prec_ctx(prec):
+            _, loss = m(x, labels=y)
         loss.backward()
         opt.step()
         opt.zero_grad()
         losses.append(loss.item())
         norms.append(opt.grad_norm.item())
     rl = np.abs(np.array(losses) - np.array(ref["losses"])) / np.array(ref["losses"])
-    assert rl.max() < 2e-2, rl
+    assert rl.max() < t_loss, rl
     rn = np.abs(np.array(norms) - np.array(ref["grad_norms"])) / np.array(ref["grad_norms"])
-    assert rn.max() < 5e-2, rn
+    assert rn.max() < t_norm, rn
 
 
 def test_torch_optimizer_and_clip_grad_norm_interop():
@@ -130,10 +151,10 @@ def test_dropout_train_vs_eval():
     assert all(torch.isfinite(p.grad).all() for p in m.parameters())
 
 
-@pytest.mark.parametrize("steps", [20])
-def test_124m_bf16_trajectory_vs_reference(steps):
-    """124M, B=4, T=1024, Zipf shards, 2 workers: bf16 loss within 2e-2 of the reference's fp32
-    CPU trajectory at every step (tests/golden/traj_124m.json)."""
+@pytest.mark.parametrize("prec", ["bf16", "fp32"])
+def test_124m_trajectory_vs_reference(prec, steps=20):
+    """124M, B=4, T=1024, Zipf shards, 2 workers: loss within 1e-4 (fp32) / 2e-2 (bf16 autocast) of
+    the reference's fp32 CPU trajectory at every one of 20 steps (tests/golden/traj_124m.json)."""
     path = os.path.join(GOLDEN, "traj_124m.json")
     if not os.path.exists(path):
         pytest.skip("traj golden missing")
@@ -148,11 +169,12 @@ def test_124m_bf16_trajectory_vs_reference(steps):
         it = D.iter_batches(D.get_shard_paths(d, "train"), 1024, 4, num_workers=2)
         for _ in range(steps):
             x, y = next(it)
-            _, loss = m(x.to(dev), labels=y.to(dev))
+            with prec_ctx(prec):
+                _, loss = m(x.to(dev), labels=y.to(dev))
             loss.backward()
             opt.step()
             opt.zero_grad()
             losses.append(loss.item())
     rl = np.abs(np.array(losses) - np.array(ref["losses"][:steps])) / np.array(ref["losses"][:steps])
-    print("max rel loss err", rl.max(), losses[0], losses[-1])
-    assert rl.max() < 2e-2, rl
+    print(prec, "max rel loss err", rl.max(), losses[0], losses[-1])
+    assert rl.max() < TOL[prec][3], rl
