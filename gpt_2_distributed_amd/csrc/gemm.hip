@@ -207,7 +207,9 @@ int launch(const GemmParams& P, int splits, hipStream_t s) {
 
 }  // namespace
 
-static int g_gemm_impl = 0;  // 0 auto, 1 force the 128x128 kernel (A/B benchmarking)
+// 0 auto (ping-pong 256x256), 1 force 128x128, 2 force the 2-stage 256x256, 3..5 ping-pong with
+// half-tile map 1..3 (A/B experiments, tools/gemm_probe.py)
+static int g_gemm_impl = 0;
 GPT2MI_EXPORT void gpt2mi_set_gemm_impl(int impl) { g_gemm_impl = impl; }
 
 // layout: 0 = forward (A[M][K], B[N][K]); 1 = dgrad (A[M][K], B[K][N]); 2 = wgrad (A[K][M], B[K][N]).
@@ -240,6 +242,10 @@ GPT2MI_EXPORT int gpt2mi_gemm(int layout, int epilogue, int M, int N, int K, con
   P.inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
   hipStream_t s = (hipStream_t)stream;
   const bool big_ok = splits == 1 && N % 256 == 0 && epilogue != EPI_ATOMIC && (layout <= 1 || M % 256 == 0);
+  if (big_ok && (g_gemm_impl == 0 || g_gemm_impl >= 3)) {
+    const int rc = gpt2mi::gemm_pp_dispatch(layout, epilogue, P, s, 1, g_gemm_impl >= 3 ? g_gemm_impl - 2 : 0);
+    if (rc >= 0) return rc;
+  }
   if (big_ok && g_gemm_impl != 1) {
     const int rc = gpt2mi::gemm256_dispatch(layout, epilogue, P, s, 1);
     if (rc >= 0) return rc;
@@ -283,13 +289,18 @@ GPT2MI_EXPORT int gpt2mi_gemm_wgrad(int M, int N, int K, const uint16_t* A, int 
   splits = (K + P.k_per_split - 1) / P.k_per_split;
   if (splits == 1) {
     P.C = C;
+    if (g_gemm_impl == 0) {
+      const int rc = gpt2mi::gemm_pp_dispatch(2, EPI_F32, P, s, 1);
+      if (rc >= 0) return rc;
+    }
     return gpt2mi::gemm256_dispatch(2, EPI_F32, P, s, 1);
   }
   GPT2MI_REQUIRE(workspace != nullptr && workspace_floats >= (size_t)splits * M * N,
                  "gemm_wgrad: workspace of %zu floats < splits*M*N = %zu", workspace_floats, (size_t)splits * M * N);
   P.C = workspace;
   P.accumulate = 0;
-  int rc = gpt2mi::gemm256_dispatch(2, EPI_SLAB, P, s, splits);
+  int rc = g_gemm_impl == 0 ? gpt2mi::gemm_pp_dispatch(2, EPI_SLAB, P, s, splits) : -1;
+  if (rc < 0) rc = gpt2mi::gemm256_dispatch(2, EPI_SLAB, P, s, splits);
   if (rc) return rc;
   return gpt2mi::splitk_reduce(workspace, splits, (size_t)M * N, C, accumulate, s);
 }

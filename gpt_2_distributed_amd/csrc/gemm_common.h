@@ -29,21 +29,22 @@ struct GemmParams {
   float inv_keep;
 };
 
-// NewGELU (model.py:63-77) with tanh(z) = 1 - 2/(exp(2z)+1)
-__device__ __forceinline__ float gelu_f(float u) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  const float z = k0 * (u + k1 * u * u * u);
-  const float t = 1.f - 2.f / (__expf(2.f * z) + 1.f);
-  return 0.5f * u * (1.f + t);
+// NewGELU (model.py:63-77): 0.5u(1 + tanh(z)), z = sqrt(2/pi)(u + 0.044715u^3), evaluated in the
+// equivalent sigmoid form u * s with s = 1/(1 + exp(-2z)) (v_exp_f32 + v_rcp_f32: the epilogues run
+// this on every fc1 output, where a division-based tanh made them VALU-bound).
+//   gelu'(u) = s * (1 + 2*sqrt(2/pi) * u * (1 - s) * (1 + 3*0.044715*u^2))
+__device__ __forceinline__ float gelu_sig(float u) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f, m2log2e = -2.0f * 1.4426950408889634f;
+  const float z = k0 * u * (1.f + k1 * u * u);
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(m2log2e * z));
 }
+__device__ __forceinline__ float gelu_f(float u) { return u * gelu_sig(u); }
 __device__ __forceinline__ float gelu_grad_f(float u) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  const float z = k0 * (u + k1 * u * u * u);
-  const float t = 1.f - 2.f / (__expf(2.f * z) + 1.f);
-  return 0.5f * (1.f + t) + 0.5f * u * (1.f - t * t) * k0 * (1.f + 3.f * k1 * u * u);
+  const float sg = gelu_sig(u);
+  return sg * (1.f + 2.f * k0 * u * (1.f - sg) * (1.f + 3.f * k1 * u * u));
 }
 
-// Apply the fused epilogue to 4 consecutive outputs C[gm][gn..gn+3]; v = alpha*acc (+bias).
 // keep mask of the 4 dropout elements didx..didx+3 (didx even): two hashes, 16 bits per element
 __device__ __forceinline__ void drop4(const GemmParams& P, uint64_t didx, bool keep[4]) {
   const uint32_t s = seed32(P.seed);
@@ -130,5 +131,6 @@ __device__ __forceinline__ void epilogue_store(const GemmParams& P, int gm, int 
 
 namespace gpt2mi {
 int gemm256_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t s, int splits);
+int gemm_pp_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t s, int splits, int map = 0);
 int splitk_reduce(const float* slab, int splits, size_t n, float* out, int accumulate, hipStream_t s);
 }

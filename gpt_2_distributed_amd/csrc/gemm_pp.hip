@@ -1,0 +1,332 @@
+// bf16 MFMA GEMM, 256x256x64 block tile, "ping-pong" 4-phase K-step — the main GEMM of the step.
+//
+// Same contract and epilogues as gemm.hip / gemm256.hip (C = epi(alpha * A.B^T), layouts 0/1/2).
+//
+// Structure (CDNA4 idiom: 2 waves per SIMD that alternate MFMA and memory work):
+//  * 512 threads = 8 waves = 2 groups of 4 (group g = wave>>2, one wave of each group per SIMD).
+//    Wave (g, c) owns a 2x2 grid of 64x32 quadrants (mi, ni): rows mi*128 + g*64..+64, columns
+//    ni*128 + c*32..+32; a quadrant x K=64 is 16 v_mfma_f32_16x16x32_bf16.
+//  * A K-tile is staged as four 16 KiB "half-tiles" A_0/A_1 (rows 0-127 / 128-255) and B_0/B_1
+//    (columns 0-127 / 128-255): contiguous 256-B global segments for m-contiguous operands. Two
+//    K-tile buffers = 128 KiB LDS, filled only by LDS-DMA (global_load_lds_dwordx4, 2 per wave per
+//    half-tile).
+//  * One K-tile = 4 phases; phase p: ds_read the quadrant's new operands, issue one half-tile DMA,
+//    s_waitcnt vmcnt(8), s_barrier, MFMA the quadrant at s_setprio 1, s_barrier. Group 1 starts one
+//    barrier late, so in every barrier interval one group runs MFMAs while the other reads LDS /
+//    issues DMA. B_0 stays in registers from phase 1 to phase 4, so every slot dies early:
+//        phase  quadrant   reads        DMA issued (into)
+//          1    (0,0)      A_0, B_0     B_1 of tile t+1   (buffer t+1; last read 3 phases ago)
+//          2    (0,1)      B_1          A_1 of tile t+1   (buffer t+1; last read 3 phases ago)
+//          3    (1,1)      A_1          A_0 of tile t+2   (buffer t, read last in phase 1)
+//          4    (1,0)      -            B_0 of tile t+2   (buffer t, read last in phase 1)
+//    Every slot is restaged >= 2 phases after its last read (WAR across the group stagger) and
+//    each half-tile is issued 5-6 phases before its first read: the counted `vmcnt(8)` of every
+//    phase keeps 4 half-tiles (64 KiB per CU) in flight across the barrier and retires exactly the
+//    half-tile the next phase reads (RAW: wait in phase p, read in phase p+1).
+//    DMA for tiles past the end re-load the last tile (never read) so the count stays static.
+//  * Operand images: k-contiguous operands [128][64] bf16 (128-B rows, 16-B chunk c at c^(row&7),
+//    ds_read_b128); m-contiguous operands [64][128] (256-B rows, chunk c at c^swz(k),
+//    ds_read_b64_tr_b16). The swizzle is applied on the DMA source address (the LDS side of an
+//    LDS-DMA is lane-linear) and undone on the read.
+//  * Epilogue through LDS: the MFMA is issued as D^T = B.A^T (a lane owns 4 consecutive columns);
+//    the block writes its fp32 accumulators into a [128][256] row-major LDS image (two passes of
+//    128 rows, 16-B chunk c of row r at c ^ (r & 15): conflict-free both ways), then every wave
+//    reads back whole rows and applies the fused epilogue with full-row coalesced stores (one
+//    store instruction = one 256-column output row).
+#include "common.h"
+#include "gemm_common.h"
+
+namespace {
+
+constexpr int BM = 256, BN = 256, BK = 64;
+constexpr int kThreads = 512;
+constexpr int kHalf = 128 * BK * 2;  // 16 KiB
+constexpr int kBuf = 4 * kHalf;      // A_0, A_1, B_0, B_1
+constexpr int kLds = 2 * kBuf;       // 128 KiB
+constexpr int SA0 = 0, SA1 = kHalf, SB0 = 2 * kHalf, SB1 = 3 * kHalf;
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+__device__ __forceinline__ int mc_swz(int k) { return 2 * ((k & 3) | (((k >> 3) & 1) << 2)); }
+
+// image row/col ir (0..127) of half `h` -> offset inside the 256-wide block dimension
+//   contiguous (default): A_h / B_h = rows / columns h*128 + ir
+//   interleaved (A/B experiments): A_h = 64-row slice h of each 128-row group, B_h = 32-column slice
+//   h of each 64-column group
+template <bool INTERLEAVED, bool IS_A>
+__device__ __forceinline__ int half_map(int ir, int h) {
+  if constexpr (!INTERLEAVED) return (h << 7) + ir;
+  else if constexpr (IS_A) return ((ir >> 6) << 7) + (h << 6) + (ir & 63);
+  else return ((ir >> 5) << 6) + (h << 5) + (ir & 31);
+}
+
+// One half-tile by LDS-DMA: 16 x 1 KiB instructions, 2 per wave.
+//   TRANS=0 (k-contiguous, src[row][k]): instruction covers image rows 8*ins..+8
+//   TRANS=1 (m-contiguous, src[k][row]): instruction covers k-rows 4*ins..+4
+template <bool TRANS, bool IS_A, bool IL>
+__device__ __forceinline__ void dma_half(const bf16* __restrict__ src, int ld, int base, int h, int k0, int rmax,
+                                         char* slot, int wid, int lane) {
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int ins = wid * 2 + t;
+    const bf16* g;
+    if constexpr (!TRANS) {
+      const int ir = 8 * ins + (lane >> 3);
+      const int c = (lane & 7) ^ (ir & 7);
+      g = src + (size_t)min(base + half_map<IL, IS_A>(ir, h), rmax) * ld + k0 + 8 * c;
+    } else {
+      const int k = 4 * ins + (lane >> 4);
+      const int c = (lane & 15) ^ mc_swz(k);
+      g = src + (size_t)(k0 + k) * ld + base + half_map<IL, IS_A>(8 * c, h);
+    }
+    __builtin_amdgcn_global_load_lds((const void*)g, (lds_void*)(slot + ins * 1024), 16, 0, 0);
+  }
+}
+
+// fragment reads: lane gets operand[ir0 + (l&15)][32kk + 8(l>>4) + 0..7]
+template <bool TRANS>
+__device__ __forceinline__ bf16x8 frag(const char* slot, int ir0, int kk, int lane) {
+  if constexpr (!TRANS) {
+    const int ir = ir0 + (lane & 15), c = 4 * kk + (lane >> 4);
+    return *reinterpret_cast<const bf16x8*>(slot + ir * 128 + 16 * (c ^ (ir & 7)));
+  } else {
+    const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+    const int k1 = 32 * kk + 8 * g + q;
+    const int chunk = (ir0 >> 3) + (p >> 1);
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_s16x4*)(slot + k1 * 256 + 16 * ((chunk ^ mc_swz(k1)) & 15) + 8 * (p & 1)));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_s16x4*)(slot + (k1 + 4) * 256 + 16 * ((chunk ^ mc_swz(k1 + 4)) & 15) + 8 * (p & 1)));
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, r);
+  }
+}
+
+struct Frags {
+  bf16x8 a[2][4];   // [kk][row frag] of the current A half
+  bf16x8 b[2][2][2];  // [ni][kk][col frag]: B_0 (kept for the whole K-tile) and B_1
+};
+
+template <bool A_T>
+__device__ __forceinline__ void read_a(Frags& f, const char* slot, int wr, int lane) {  // image rows wr*64..+64
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) f.a[kk][i] = frag<A_T>(slot, wr * 64 + 16 * i, kk, lane);
+}
+template <bool B_T, int NI>
+__device__ __forceinline__ void read_b(Frags& f, const char* slot, int wc, int lane) {
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) f.b[NI][kk][j] = frag<B_T>(slot, wc * 32 + 16 * j, kk, lane);
+}
+
+template <int NI>
+__device__ __forceinline__ void mfma_quadrant(f32x4 (&acc)[4][2], const Frags& f) {
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.b[NI][kk][j], f.a[kk][i], acc[i][j], 0, 0, 0);
+}
+
+// end of a phase's memory segment: retire the half-tile the next phase reads, then the ping-pong
+// MFMA segment between two barriers
+#define PP_SYNC_MFMA(ACC, NI)                              \
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");         \
+  __builtin_amdgcn_sched_barrier(0);                       \
+  __builtin_amdgcn_s_barrier();                            \
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");       \
+  __builtin_amdgcn_sched_barrier(0);                       \
+  __builtin_amdgcn_s_setprio(1);                           \
+  mfma_quadrant<NI>(ACC, fr);                              \
+  __builtin_amdgcn_s_setprio(0);                           \
+  __builtin_amdgcn_sched_barrier(0);                       \
+  __builtin_amdgcn_s_barrier();                            \
+  __builtin_amdgcn_sched_barrier(0);
+
+// workgroup barrier that orders LDS only (the epilogue's global stores stay in flight)
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <bool A_T, bool B_T, int EPI, int MAP>
+__global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
+  constexpr bool AIL = MAP & 1, BIL = MAP & 2;  // interleaved half-tile maps (A/B experiments)
+  __shared__ __attribute__((aligned(1024))) char smem[kLds];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+
+  const int tiles_m = (P.M + BM - 1) / BM, tiles_n = P.N / BN;
+  const int ntiles = tiles_m * tiles_n;
+  const int pid = xcd_remap(blockIdx.x, ntiles);
+  constexpr int GM = 4;
+  const int group = pid / (GM * tiles_n);
+  const int first_m = group * GM;
+  const int gsz = min(tiles_m - first_m, GM);
+  const int tm = first_m + (pid % (GM * tiles_n)) % gsz;
+  const int tn = (pid % (GM * tiles_n)) / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kbeg = blockIdx.y * P.k_per_split;
+  const int nk = (min(P.K, kbeg + P.k_per_split) - kbeg) / BK;  // even (host-checked)
+
+  f32x4 acc[2][2][4][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto kofs = [&](int t) { return kbeg + min(t, nk - 1) * BK; };
+  auto dma_a = [&](int t, int h, char* buf) {
+    dma_half<A_T, true, AIL>(P.A, P.lda, m0, h, kofs(t), P.M - 1, buf + (h ? SA1 : SA0), wid, lane);
+  };
+  auto dma_b = [&](int t, int h, char* buf) {
+    dma_half<B_T, false, BIL>(P.B, P.ldb, n0, h, kofs(t), P.N - 1, buf + (h ? SB1 : SB0), wid, lane);
+  };
+  char* buf0 = smem;
+  char* buf1 = smem + kBuf;
+
+  // prologue: what phases -6..-1 would have issued (all of tile 0, A_0 / B_0 of tile 1), in order
+  dma_a(0, 0, buf0);
+  dma_b(0, 0, buf0);
+  dma_b(0, 1, buf0);
+  dma_a(0, 1, buf0);
+  dma_a(1, 0, buf1);
+  dma_b(1, 0, buf1);
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A_0(0), B_0(0) landed
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind group 0
+  __builtin_amdgcn_sched_barrier(0);
+
+  Frags fr;
+  for (int t = 0; t < nk; t += 2) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      char* cur = s ? buf1 : buf0;
+      char* nxt = s ? buf0 : buf1;
+      const int tt = t + s;
+      // phase 1: quadrant (0,0)
+      read_a<A_T>(fr, cur + SA0, wr, lane);
+      read_b<B_T, 0>(fr, cur + SB0, wc, lane);
+      dma_b(tt + 1, 1, nxt);
+      PP_SYNC_MFMA(acc[0][0], 0)
+      // phase 2: quadrant (0,1)
+      read_b<B_T, 1>(fr, cur + SB1, wc, lane);
+      dma_a(tt + 1, 1, nxt);
+      PP_SYNC_MFMA(acc[0][1], 1)
+      // phase 3: quadrant (1,1)
+      read_a<A_T>(fr, cur + SA1, wr, lane);
+      dma_a(tt + 2, 0, cur);
+      PP_SYNC_MFMA(acc[1][1], 1)
+      // phase 4: quadrant (1,0) from registers
+      dma_b(tt + 2, 0, cur);
+      PP_SYNC_MFMA(acc[1][0], 0)
+    }
+  }
+  if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the groups (same barrier count)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail DMAs into LDS have landed
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+
+  // ---- epilogue: acc[mi][ni][i][j][r] = C[m0 + mi*128 + wr*64 + 16i + (l&15)][n0 + ni*128 + wc*32 + 16j + 4(l>>4) + r]
+  float alpha = P.alpha;
+  if (P.alpha_dev) alpha *= P.alpha_dev[0];
+  float* img = reinterpret_cast<float*>(smem);  // [128][256] fp32, 1 KiB rows
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi) {
+    if (mi) lds_barrier();  // pass 0's reads are done before pass 1 overwrites the image
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int r = wr * 64 + 16 * i + (lane & 15);
+          const int ch = BIL ? wc * 16 + ni * 8 + 4 * j + (lane >> 4) : ni * 32 + wc * 8 + 4 * j + (lane >> 4);
+          f32x4 v = acc[mi][ni][i][j];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] *= alpha;
+          *reinterpret_cast<f32x4*>(img + r * 256 + 4 * (ch ^ (r & 15))) = v;
+        }
+    lds_barrier();
+    const int ch = tid & 63;
+    const int gn = n0 + 4 * ch;
+    const f32x4 bias = (P.bias && EPI != EPI_GELU_BWD) ? *reinterpret_cast<const f32x4*>(P.bias + gn)
+                                                       : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+    for (int it = 0; it < 16; ++it) {
+      const int r = it * 8 + (tid >> 6);
+      const int gm = m0 + (AIL ? ((r >> 6) << 7) + mi * 64 + (r & 63) : mi * 128 + r);
+      f32x4 v = *reinterpret_cast<const f32x4*>(img + r * 256 + 4 * (ch ^ (r & 15)));
+      if (gm >= P.M) continue;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] += bias[e];
+      if constexpr (EPI == EPI_SLAB) {
+        float* slab = reinterpret_cast<float*>(P.C) + (size_t)blockIdx.y * P.M * P.ldc;
+        *reinterpret_cast<f32x4*>(slab + (size_t)gm * P.ldc + gn) = v;
+      } else {
+        epilogue_store<EPI>(P, gm, gn, v);
+      }
+    }
+  }
+}
+
+// Default half-tile maps: interleaved for m-contiguous (transposed) operands, contiguous otherwise
+// (measured, tools/gemm_probe.py: 8192^3 dgrad 1195 vs 1022 TF with B interleaved; no effect on the
+// k-contiguous forward operands).
+template <bool A_T, bool B_T, int EPI, int MAP = (A_T ? 1 : 0) | (B_T ? 2 : 0)>
+int launch(const GemmParams& P, hipStream_t s, int splits) {
+  dim3 grid(((P.M + BM - 1) / BM) * (P.N / BN), splits);
+  gemm_pp_kernel<A_T, B_T, EPI, MAP><<<grid, kThreads, 0, s>>>(P);
+  return gpt2mi::check_launch("gemm_pp");
+}
+
+}  // namespace
+
+namespace gpt2mi {
+// N % 256 == 0, every split's K range an even number (>= 2) of 64-deep tiles; layout 2 needs M % 256 == 0.
+// Returns -1 when this kernel does not apply (the caller falls back).
+int gemm_pp_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t s, int splits, int map) {
+  if (P.N % BN != 0 || P.k_per_split % (2 * BK) != 0 || P.K % (2 * BK) != 0) return -1;
+  // measured slower than the 2-stage gemm256 kernel (tools/gemm_probe.py): the wgrad instantiations
+  // spill at 256 VGPRs, and the GELU-backward epilogue is bound by its aux-load latency
+  if (map == 0 && (layout == 2 || epilogue == EPI_GELU_BWD)) return -1;
+  if (layout == 2 && P.M % BM != 0) return -1;
+  if (map > 0 && epilogue == EPI_BF16 && layout <= 1) {  // half-tile map experiments (tools/gemm_probe.py)
+    if (layout == 0) {
+      if (map == 1) return launch<false, false, EPI_BF16, 1>(P, s, 1);
+      if (map == 2) return launch<false, false, EPI_BF16, 2>(P, s, 1);
+      if (map == 3) return launch<false, false, EPI_BF16, 3>(P, s, 1);
+    } else {
+      if (map == 1) return launch<false, true, EPI_BF16, 1>(P, s, 1);
+      if (map == 2) return launch<false, true, EPI_BF16, 2>(P, s, 1);
+      if (map == 3) return launch<false, true, EPI_BF16, 3>(P, s, 1);
+    }
+  }
+  switch (layout * 16 + epilogue) {
+    case 0 * 16 + EPI_BF16: return launch<false, false, EPI_BF16>(P, s, 1);
+    case 0 * 16 + EPI_F32: return launch<false, false, EPI_F32>(P, s, 1);
+    case 0 * 16 + EPI_RESID: return launch<false, false, EPI_RESID>(P, s, 1);
+    case 0 * 16 + EPI_GELU: return launch<false, false, EPI_GELU>(P, s, 1);
+    case 1 * 16 + EPI_BF16: return launch<false, true, EPI_BF16>(P, s, 1);
+    case 1 * 16 + EPI_F32: return launch<false, true, EPI_F32>(P, s, 1);
+    case 1 * 16 + EPI_GELU_BWD: return launch<false, true, EPI_GELU_BWD>(P, s, 1);
+    case 2 * 16 + EPI_F32: return launch<true, true, EPI_F32>(P, s, 1);
+    case 2 * 16 + EPI_SLAB: return launch<true, true, EPI_SLAB>(P, s, splits);
+    default: return -1;
+  }
+}
+}  // namespace gpt2mi

@@ -339,7 +339,8 @@ def test_colsum():
 
 @pytest.mark.parametrize("layout,epi", [(0, 0), (0, 2), (0, 3), (1, 0), (1, 4)])
 def test_gemm256_matches_gemm128(layout, epi):
-    """The 256x256 LDS-DMA kernel and the 128x128 kernel agree on every fused epilogue (incl. dropout)."""
+    """The ping-pong 256x256, 2-stage 256x256 and 128x128 kernels agree on every fused epilogue (incl.
+    dropout)."""
     M, N, K = 320, 768, 192  # partial 256-row tile
     g = torch.Generator().manual_seed(layout * 10 + epi)
     A = bf(torch.randn(M, K, generator=g)).to(dev)
@@ -348,7 +349,7 @@ def test_gemm256_matches_gemm128(layout, epi):
     bias = torch.randn(N, generator=g).to(dev)
     resid = torch.randn(M, N, generator=g).to(dev)
     outs = []
-    for impl in (0, 1):
+    for impl in (0, 1, 2):
         L().set_gemm_impl(impl)
         f32 = epi == 2
         C = torch.zeros(M, N, device=dev, dtype=torch.float32 if f32 else torch.bfloat16)
@@ -357,11 +358,13 @@ def test_gemm256_matches_gemm128(layout, epi):
                  resid=resid if epi == 2 else None, aux=aux, ldaux=N, p_drop=0.1, seed=77)
         outs.append((C.float().cpu(), aux.float().cpu()))
     L().set_gemm_impl(0)
-    assert rel_err(outs[0][0], outs[1][0]) < 1e-5 if epi == 2 else rel_err(outs[0][0], outs[1][0]) < 2e-3
-    assert rel_err(outs[0][1], outs[1][1]) < 2e-3
+    for o in outs[1:]:
+        assert rel_err(outs[0][0], o[0]) < 1e-5 if epi == 2 else rel_err(outs[0][0], o[0]) < 2e-3
+        assert rel_err(outs[0][1], o[1]) < 2e-3
 
 
-@pytest.mark.parametrize("M,N,K,splits", [(256, 256, 1024, 1), (512, 768, 4096, 7), (768, 256, 2048, 3)])
+@pytest.mark.parametrize("M,N,K,splits", [(256, 256, 1024, 1), (512, 768, 4096, 7), (768, 256, 2048, 3),
+                                          (768, 512, 4096, 4), (256, 768, 3072, 1)])
 def test_gemm_wgrad_splitk_slabs(M, N, K, splits):
     g = torch.Generator().manual_seed(M + N + splits)
     A, B = bf(torch.randn(K, M, generator=g)), bf(torch.randn(K, N, generator=g))
@@ -374,3 +377,18 @@ def test_gemm_wgrad_splitk_slabs(M, N, K, splits):
     C2 = C0.to(dev)
     L().gemm_wgrad(M, N, K, A.to(dev), M, B.to(dev), N, C2, N, accumulate=True, alpha=0.5, workspace=ws, splits=splits)
     assert torch.equal(C, C2)
+
+
+@pytest.mark.parametrize("layout", [0, 1])
+@pytest.mark.parametrize("M,N,K", [(512, 768, 768), (448, 512, 1024), (256, 2304, 128)])
+def test_gemm_pingpong_vs_fp64(layout, M, N, K):
+    """The ping-pong kernel (default for N % 256 == 0, even K-tile count) against an fp64 reference:
+    full tiles, a partial last row tile, the shortest K (2 K-tiles) and GPT-2 widths."""
+    g = torch.Generator().manual_seed(M + N + K + layout)
+    A = bf(torch.randn(M, K, generator=g))
+    B = bf(torch.randn(N, K, generator=g) if layout == 0 else torch.randn(K, N, generator=g))
+    ref = A.double() @ (B.double().t() if layout == 0 else B.double())
+    C = torch.full((M, N), 3.0, device=dev)
+    L().gemm(layout, L().EPI_F32, M, N, K, A.to(dev), K, B.to(dev), B.shape[1], C, N, alpha=0.25)
+    torch.cuda.synchronize()
+    assert rel_err(C.cpu(), 0.25 * ref) < 1e-6

@@ -105,8 +105,9 @@ if __name__ == "__main__":
         attn(p=0.0)
         attn(p=0.1)
     if "gemm" in what:
-        for impl in (0, 1):
-            print(f"--- gemm impl {impl} ({ {0: '256x256 where it applies', 1: '128x128 only'}[impl] })")
+        impls = [int(a[5:]) for a in sys.argv[1:] if a.startswith("impl=")] or [0, 2]
+        for impl in impls:
+            print(f"--- gemm impl {impl} ({ {0: 'ping-pong 256x256', 1: '128x128 only', 2: '2-stage 256x256'}[impl] })")
             K.set_gemm_impl(impl)
             gemm()
         K.set_gemm_impl(0)
