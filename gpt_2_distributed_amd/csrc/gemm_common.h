@@ -72,10 +72,27 @@ __device__ __forceinline__ f32x4 load4(const TE* p) {
   }
 }
 
-// Apply the fused epilogue to 4 consecutive outputs C[gm][gn..gn+3]; v = alpha*acc (+bias).
-// TE = element type of the bf16-or-fp32 outputs (C of BF16/GELU/GELU_BWD, aux).
+// The epilogue's input operand at C[gm][gn..gn+3]: the residual (RESID), the stored pre-activation
+// (GELU_BWD) or the old C (F32 with accumulate); zeros otherwise. Separate from the apply step so a
+// kernel can issue these loads early (gemm_pp.hip prefetches a whole pass of them).
 template <int EPI, typename TE = bf16>
-__device__ __forceinline__ void epilogue_store(const GemmParams& P, int gm, int gn, f32x4 v) {
+__device__ __forceinline__ f32x4 epilogue_operand(const GemmParams& P, int gm, int gn) {
+  if constexpr (EPI == EPI_RESID) {
+    return *reinterpret_cast<const f32x4*>(P.resid + (size_t)gm * P.ldc + gn);
+  } else if constexpr (EPI == EPI_GELU_BWD) {
+    return load4<TE>(reinterpret_cast<const TE*>(P.aux) + (size_t)gm * P.ldaux + gn);
+  } else if constexpr (EPI == EPI_F32) {
+    if (P.accumulate) return *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(P.C) + (size_t)gm * P.ldc + gn);
+    return f32x4{0.f, 0.f, 0.f, 0.f};
+  } else {
+    return f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+}
+
+// Apply the fused epilogue to 4 consecutive outputs C[gm][gn..gn+3]; v = alpha*acc (+bias), opnd =
+// epilogue_operand(gm, gn). TE = element type of the bf16-or-fp32 outputs (C of BF16/GELU/GELU_BWD, aux).
+template <int EPI, typename TE = bf16>
+__device__ __forceinline__ void epilogue_apply(const GemmParams& P, int gm, int gn, f32x4 v, f32x4 opnd) {
   const size_t cidx = (size_t)gm * P.ldc + gn;
   const uint64_t didx = (uint64_t)gm * P.N + gn;  // dropout element index in the logical [M,N] (even)
   bool keep[4] = {true, true, true, true};
@@ -84,23 +101,17 @@ __device__ __forceinline__ void epilogue_store(const GemmParams& P, int gm, int 
   if constexpr (EPI == EPI_BF16) {
     store4<TE>(reinterpret_cast<TE*>(P.C) + cidx, v);
   } else if constexpr (EPI == EPI_F32) {
-    float* C = reinterpret_cast<float*>(P.C);
-    if (P.accumulate) {
-      f32x4 o = *reinterpret_cast<const f32x4*>(C + cidx);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] += o[j];
-    }
-    *reinterpret_cast<f32x4*>(C + cidx) = v;
+    for (int j = 0; j < 4; ++j) v[j] += opnd[j];
+    *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(P.C) + cidx) = v;
   } else if constexpr (EPI == EPI_RESID) {
-    float* C = reinterpret_cast<float*>(P.C);
-    f32x4 r = *reinterpret_cast<const f32x4*>(P.resid + cidx);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       float y = v[j];
       if (P.thr) y = keep[j] ? y * P.inv_keep : 0.f;
-      r[j] += y;
+      opnd[j] += y;
     }
-    *reinterpret_cast<f32x4*>(C + cidx) = r;
+    *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(P.C) + cidx) = opnd;
   } else if constexpr (EPI == EPI_GELU) {
     f32x4 h;
 #pragma unroll
@@ -113,13 +124,12 @@ __device__ __forceinline__ void epilogue_store(const GemmParams& P, int gm, int 
     store4<TE>(reinterpret_cast<TE*>(P.C) + cidx, h);
   } else if constexpr (EPI == EPI_GELU_BWD) {
     // gelu' is evaluated at the STORED pre-activation (bf16-rounded under autocast), as autograd does
-    const f32x4 u = load4<TE>(reinterpret_cast<const TE*>(P.aux) + (size_t)gm * P.ldaux + gn);
     f32x4 o;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       float d = v[j];
       if (P.thr) d = keep[j] ? d * P.inv_keep : 0.f;
-      o[j] = d * gelu_grad_f(u[j]);
+      o[j] = d * gelu_grad_f(opnd[j]);
     }
     store4<TE>(reinterpret_cast<TE*>(P.C) + cidx, o);
   } else if constexpr (EPI == EPI_ATOMIC) {
@@ -127,6 +137,11 @@ __device__ __forceinline__ void epilogue_store(const GemmParams& P, int gm, int 
 #pragma unroll
     for (int j = 0; j < 4; ++j) atomicAdd(C + cidx + j, v[j]);
   }
+}
+
+template <int EPI, typename TE = bf16>
+__device__ __forceinline__ void epilogue_store(const GemmParams& P, int gm, int gn, f32x4 v) {
+  epilogue_apply<EPI, TE>(P, gm, gn, v, epilogue_operand<EPI, TE>(P, gm, gn));
 }
 
 namespace gpt2mi {

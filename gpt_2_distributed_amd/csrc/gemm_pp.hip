@@ -245,8 +245,24 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   if (P.alpha_dev) alpha *= P.alpha_dev[0];
   float* img = reinterpret_cast<float*>(smem);  // [128][256] fp32, 1 KiB rows
   const int tid = threadIdx.x;
+  const int ch = tid & 63;
+  const int gn = n0 + 4 * ch;
+  const f32x4 bias = (P.bias && EPI != EPI_GELU_BWD) ? *reinterpret_cast<const f32x4*>(P.bias + gn)
+                                                     : f32x4{0.f, 0.f, 0.f, 0.f};
+  constexpr bool kOpnd = EPI == EPI_RESID || EPI == EPI_GELU_BWD || EPI == EPI_F32;
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi) {
+    // the pass's epilogue operands (residual / pre-activation / old C): all 16 loads in flight
+    // while the accumulators go through LDS
+    f32x4 opnd[16];
+    if constexpr (kOpnd) {
+#pragma unroll
+      for (int it = 0; it < 16; ++it) {
+        const int r = it * 8 + (tid >> 6);
+        const int gm = m0 + (AIL ? ((r >> 6) << 7) + mi * 64 + (r & 63) : mi * 128 + r);
+        opnd[it] = epilogue_operand<EPI>(P, min(gm, P.M - 1), gn);
+      }
+    }
     if (mi) lds_barrier();  // pass 0's reads are done before pass 1 overwrites the image
 #pragma unroll
     for (int ni = 0; ni < 2; ++ni)
@@ -255,30 +271,42 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const int r = wr * 64 + 16 * i + (lane & 15);
-          const int ch = BIL ? wc * 16 + ni * 8 + 4 * j + (lane >> 4) : ni * 32 + wc * 8 + 4 * j + (lane >> 4);
+          const int c = BIL ? wc * 16 + ni * 8 + 4 * j + (lane >> 4) : ni * 32 + wc * 8 + 4 * j + (lane >> 4);
           f32x4 v = acc[mi][ni][i][j];
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] *= alpha;
-          *reinterpret_cast<f32x4*>(img + r * 256 + 4 * (ch ^ (r & 15))) = v;
+          *reinterpret_cast<f32x4*>(img + r * 256 + 4 * (c ^ (r & 15))) = v;
         }
     lds_barrier();
-    const int ch = tid & 63;
-    const int gn = n0 + 4 * ch;
-    const f32x4 bias = (P.bias && EPI != EPI_GELU_BWD) ? *reinterpret_cast<const f32x4*>(P.bias + gn)
-                                                       : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-    for (int it = 0; it < 16; ++it) {
+    auto row_of = [&](int it) {
       const int r = it * 8 + (tid >> 6);
-      const int gm = m0 + (AIL ? ((r >> 6) << 7) + mi * 64 + (r & 63) : mi * 128 + r);
-      f32x4 v = *reinterpret_cast<const f32x4*>(img + r * 256 + 4 * (ch ^ (r & 15)));
-      if (gm >= P.M) continue;
+      return m0 + (AIL ? ((r >> 6) << 7) + mi * 64 + (r & 63) : mi * 128 + r);
+    };
+    auto finish = [&](int it, f32x4 v) {
+      const int gm = row_of(it);
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] += bias[e];
       if constexpr (EPI == EPI_SLAB) {
         float* slab = reinterpret_cast<float*>(P.C) + (size_t)blockIdx.y * P.M * P.ldc;
         *reinterpret_cast<f32x4*>(slab + (size_t)gm * P.ldc + gn) = v;
       } else {
-        epilogue_store<EPI>(P, gm, gn, v);
+        epilogue_apply<EPI>(P, gm, gn, v, kOpnd ? opnd[it] : f32x4{0.f, 0.f, 0.f, 0.f});
+      }
+    };
+    if (m0 + BM <= P.M) {  // full tile (block-uniform): straight-line reads, then the stores
+      f32x4 v[16];
+#pragma unroll
+      for (int it = 0; it < 16; ++it) {
+        const int r = it * 8 + (tid >> 6);
+        v[it] = *reinterpret_cast<const f32x4*>(img + r * 256 + 4 * (ch ^ (r & 15)));
+      }
+#pragma unroll
+      for (int it = 0; it < 16; ++it) finish(it, v[it]);
+    } else {
+      for (int it = 0; it < 16; ++it) {
+        const int r = it * 8 + (tid >> 6);
+        const f32x4 v = *reinterpret_cast<const f32x4*>(img + r * 256 + 4 * (ch ^ (r & 15)));
+        if (row_of(it) < P.M) finish(it, v);
       }
     }
   }
@@ -303,7 +331,7 @@ int gemm_pp_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t 
   if (P.N % BN != 0 || P.k_per_split % (2 * BK) != 0 || P.K % (2 * BK) != 0) return -1;
   // measured slower than the 2-stage gemm256 kernel (tools/gemm_probe.py): the wgrad instantiations
   // spill at 256 VGPRs, and the GELU-backward epilogue is bound by its aux-load latency
-  if (map == 0 && (layout == 2 || epilogue == EPI_GELU_BWD)) return -1;
+  if (map == 0 && layout == 2) return -1;
   if (layout == 2 && P.M % BM != 0) return -1;
   if (map > 0 && epilogue == EPI_BF16 && layout <= 1) {  // half-tile map experiments (tools/gemm_probe.py)
     if (layout == 0) {

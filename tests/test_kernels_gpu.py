@@ -275,13 +275,15 @@ def test_attention_dropout_stats_and_grad_consistency():
     # O is linear in V for fixed mask/P: <dO, O> == <dV, V>
     o = outs[0]
     L().attn_fwd(qd, o, lse, B, T, H, D, p, 1000)
-    dout = bf(torch.randn(B * T, C)).to(dev)
+    dout = bf(torch.randn(B * T, C, generator=torch.Generator().manual_seed(10))).to(dev)
     dqkv = torch.empty(B * T, 3 * C, dtype=torch.bfloat16, device=dev)
     delta = torch.empty(B * H, T, device=dev)
     L().attn_bwd(qd, o, dout, lse, delta, dqkv, B, T, H, D, p, 1000)
     lhs = (dout.float() * o.float()).sum().item()
     rhs = (dqkv[:, 2 * C:].float() * qd[:, 2 * C:].float()).sum().item()
-    assert abs(lhs - rhs) / abs(lhs) < 2e-2
+    # the sum cancels heavily: compare against the magnitude of its terms (bf16 dV rounding)
+    scale = (dout.float() * o.float()).abs().sum().item()
+    assert abs(lhs - rhs) < 2e-3 * scale, (lhs, rhs, scale)
 
 
 @pytest.mark.parametrize("M,V,ld", [(64, 509, 512), (128, 50257, 50304)])
