@@ -21,6 +21,8 @@
 //                  with P/dS from registers and dO^T/Q^T by transposed LDS reads.
 // LDS tiles are [64 rows][64 bf16] (128-B rows), 16-B chunk c stored at c ^ (row & 6): conflict-
 // free for both the ds_read_b128 row reads and the permuted transposed reads.
+#include <type_traits>
+
 #include "common.h"
 
 namespace {
@@ -56,6 +58,22 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* base, int kk, int c0, int 
   return __builtin_bit_cast(bf16x8, r);
 }
 
+// max / sum over the 4 lanes l, l^16, l^32, l^48 (one query's keys in the S^T accumulators) with
+// the VALU lane swaps of gfx950 (no LDS round trip): op(swap[0], swap[1]) = op(own, partner)
+__device__ __forceinline__ float xor_max(float v) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+__device__ __forceinline__ float xor_sum(float v) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+constexpr float kRescaleThr = 8.f;  // log2 units: P <= 256 between rescales (bf16-exact exponent range)
+
 // pack accumulator registers acc[2kk + (j>>2)][j&3] (j = 0..7) to a bf16 operand fragment
 __device__ __forceinline__ bf16x8 pack_perm(const f32x4* acc, int kk) {
   bf16x8 r;
@@ -84,7 +102,7 @@ __device__ __forceinline__ void tile_store(char* base, const u32x4* r) {
 // drop_hash(seed, (bh*T + (q & ~16))*T + key) — queries q and q^16 of one key share a hash.
 
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
+__global__ __launch_bounds__(kThreads, 3) void attn_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
                                                                float* __restrict__ lse, int T, int H, float scale,
                                                                uint64_t seed, uint32_t thr, float inv_keep) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * BKV * 128];  // 2 stages x (K, V)
@@ -160,29 +178,34 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const bf16* __res
 #pragma unroll
         for (int fi = 0; fi < 4; ++fi)
           tmax = fmaxf(tmax, fmaxf(fmaxf(s[qg][fi][0], s[qg][fi][1]), fmaxf(s[qg][fi][2], s[qg][fi][3])));
-        tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-        tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-        const float mn = fmaxf(m[qg], tmax * sl2);  // finite: tile 0 holds key 0, visible to every query
-        const float corr = exp2f(m[qg] - mn);
-        float rs = 0.f;
+        tmax = xor_max(tmax);
+        // thresholded rescale (defer-max): keep the running max unless some row of the wave grew by
+        // more than kRescaleThr (log2 units); P then stays below 2^kRescaleThr. Wave-uniform decision,
+        // taken before this tile is exponentiated, so O, l and P all see the same max.
+        const float cand = tmax * sl2;
+        if (!__all(cand <= m[qg] + kRescaleThr)) {
+          const float mn = fmaxf(m[qg], cand);  // finite: tile 0 holds key 0, visible to every query
+          const float corr = __builtin_amdgcn_exp2f(m[qg] - mn);
+          l[qg] *= corr;
+#pragma unroll
+          for (int f = 0; f < 4; ++f)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[qg][f][r] *= corr;
+          m[qg] = mn;
+        }
+        float rs = 0.f;  // per-lane partial row sum (the cross-lane sum is taken once, at the end)
 #pragma unroll
         for (int fi = 0; fi < 4; ++fi)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float p = exp2f(fmaf(s[qg][fi][r], sl2, -mn));
-            rs += p;
-            s[qg][fi][r] = p;
+            const float pv = __builtin_amdgcn_exp2f(fmaf(s[qg][fi][r], sl2, -m[qg]));
+            rs += pv;
+            s[qg][fi][r] = pv;
           }
-        rs += __shfl_xor(rs, 16, 64);
-        rs += __shfl_xor(rs, 32, 64);
-        l[qg] = l[qg] * corr + rs;
-        m[qg] = mn;
-#pragma unroll
-        for (int f = 0; f < 4; ++f)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) o[qg][f][r] *= corr;
+        l[qg] += rs;
       }
-      if (thr) {  // dropout on P (not on the normaliser): one hash per (q, q^16) pair of a key
+      if (thr) {  // dropout on P (not on the normaliser; the 1/(1-p) goes into the final scale): one
+                  // hash per (q, q^16) pair of a key
         const uint32_t s32 = seed32(seed);
         const uint32_t pbase = ((uint32_t)bh * T + q_lo + (lane & 15)) * (uint32_t)T + k_lo + 4 * g;
 #pragma unroll
@@ -190,8 +213,8 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const bf16* __res
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const uint32_t hh = drop_hash(s32, pbase + 16 * fi + r);
-            s[0][fi][r] = drop_keep16(hh, 0, thr) ? s[0][fi][r] * inv_keep : 0.f;
-            s[1][fi][r] = drop_keep16(hh, 1, thr) ? s[1][fi][r] * inv_keep : 0.f;
+            if (!drop_keep16(hh, 0, thr)) s[0][fi][r] = 0.f;
+            if (!drop_keep16(hh, 1, thr)) s[1][fi][r] = 0.f;
           }
       }
 #pragma unroll
@@ -216,7 +239,8 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const bf16* __res
 #pragma unroll
   for (int qg = 0; qg < 2; ++qg) {
     const int q = q_lo + 16 * qg + (lane & 15);
-    const float il = 1.f / l[qg];
+    l[qg] = xor_sum(l[qg]);
+    const float il = (thr ? inv_keep : 1.f) / l[qg];
     bf16* op = out + ((size_t)b * T + q) * C + h * D;
 #pragma unroll
     for (int fd = 0; fd < 4; ++fd)
@@ -247,6 +271,7 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16* __restrict_
 
 // ---------------------------------------------------------------------------------------------
 // dQ: query-outer; recomputes P from the saved LSE. dS^T = P^T o (dP^T - delta), dQ^T += K^T dS^T.
+template <bool DROP>
 __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const bf16* __restrict__ qkv,
                                                                   const bf16* __restrict__ dout,
                                                                   const float* __restrict__ lse,
@@ -272,6 +297,10 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const bf16* __
     for (int kk = 0; kk < 2; ++kk) {
       qf[qg][kk] = *reinterpret_cast<const bf16x8*>(base + (size_t)q * ld + h * D + 32 * kk + 8 * g);
       df[qg][kk] = *reinterpret_cast<const bf16x8*>(dout + ((size_t)b * T + q) * C + h * D + 32 * kk + 8 * g);
+      if (DROP) {  // dP' = (dO/(1-p)).V: the keep-scale of dropout folded into dO once per wave
+#pragma unroll
+        for (int e = 0; e < 8; ++e) df[qg][kk][e] = f2bf(bf2f(df[qg][kk][e]) * inv_keep);
+      }
     }
     lse2[qg] = lse[(size_t)bh * T + q] * kLog2e;
     dl[qg] = delta[(size_t)bh * T + q];
@@ -318,28 +347,32 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const bf16* __
           }
         }
       }
-      if (thr) {  // dropped entries get dP = 0 (same (q, q^16)-pair hash as the forward)
-        const uint32_t s32 = seed32(seed);
-        const uint32_t pbase = ((uint32_t)bh * T + q_lo + (lane & 15)) * (uint32_t)T + k_lo + 4 * g;
+      // dS^T = P^T o (dP'^T - delta): dropped entries get dP = 0 (same (q, q^16)-pair hash as the forward)
+      auto elementwise = [&](auto diag_c) {
+        constexpr bool DIAG = decltype(diag_c)::value;
+        uint32_t pbase = 0, s32 = 0;
+        if constexpr (DROP) {
+          s32 = seed32(seed);
+          pbase = ((uint32_t)bh * T + q_lo + (lane & 15)) * (uint32_t)T + k_lo + 4 * g;
+        }
 #pragma unroll
         for (int fi = 0; fi < 4; ++fi)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const uint32_t hh = drop_hash(s32, pbase + 16 * fi + r);
-            dp[0][fi][r] = drop_keep16(hh, 0, thr) ? dp[0][fi][r] * inv_keep : 0.f;
-            dp[1][fi][r] = drop_keep16(hh, 1, thr) ? dp[1][fi][r] * inv_keep : 0.f;
+            uint32_t hh = 0;
+            if constexpr (DROP) hh = drop_hash(s32, pbase + 16 * fi + r);
+#pragma unroll
+            for (int qg = 0; qg < 2; ++qg) {
+              float p = __builtin_amdgcn_exp2f(fmaf(s[qg][fi][r], sl2, -lse2[qg]));
+              if constexpr (DIAG) p = (k_lo + 16 * fi + 4 * g + r > q_lo + 16 * qg + (lane & 15)) ? 0.f : p;
+              float d = dp[qg][fi][r];
+              if constexpr (DROP) d = drop_keep16(hh, qg, thr) ? d : 0.f;
+              s[qg][fi][r] = p * (d - dl[qg]);
+            }
           }
-      }
-#pragma unroll
-      for (int qg = 0; qg < 2; ++qg)
-#pragma unroll
-        for (int fi = 0; fi < 4; ++fi)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float p = exp2f(fmaf(s[qg][fi][r], sl2, -lse2[qg]));
-            if (diag && k_lo + 16 * fi + 4 * g + r > q_lo + 16 * qg + (lane & 15)) p = 0.f;
-            s[qg][fi][r] = p * (dp[qg][fi][r] - dl[qg]);  // dS^T
-          }
+      };
+      if (diag) elementwise(std::true_type{});
+      else elementwise(std::false_type{});
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         const bf16x8 s0 = pack_perm(s[0], kk), s1 = pack_perm(s[1], kk);
@@ -373,6 +406,7 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const bf16* __
 
 // ---------------------------------------------------------------------------------------------
 // dK, dV: key-outer (128 keys per workgroup, 32 per wave) over 64-query tiles at or after the keys.
+template <bool DROP>
 __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dkdv_kernel(const bf16* __restrict__ qkv,
                                                                     const bf16* __restrict__ dout,
                                                                     const float* __restrict__ lse,
@@ -399,6 +433,10 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dkdv_kernel(const bf16* 
       const size_t row = (size_t)min(k_lo + 16 * kg + (lane & 15), T - 1) * ld;
       kf[kg][kk] = *reinterpret_cast<const bf16x8*>(base + row + C + h * D + 32 * kk + 8 * g);
       vf[kg][kk] = *reinterpret_cast<const bf16x8*>(base + row + 2 * C + h * D + 32 * kk + 8 * g);
+      if (DROP) {  // dP' = dO.(V/(1-p)): the keep-scale of dropout folded into V once per wave
+#pragma unroll
+        for (int e = 0; e < 8; ++e) vf[kg][kk][e] = f2bf(bf2f(vf[kg][kk][e]) * inv_keep);
+      }
     }
   const float sl2 = scale * kLog2e;
   f32x4 dk[2][4], dv[2][4];
@@ -470,28 +508,35 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dkdv_kernel(const bf16* 
           l4[fl] = *reinterpret_cast<const f32x4*>(Ls + 16 * (2 * hq + fl) + 4 * g);
           d4[fl] = *reinterpret_cast<const f32x4*>(Dl + 16 * (2 * hq + fl) + 4 * g);
         }
+        // P = exp2(S*scale*log2e - LSE*log2e); dropped entries: P_drop = 0 (dV; its 1/(1-p) is applied
+        // to dV at the end) and dP = 0 (dS); dP already carries 1/(1-p) through the prescaled V.
+        auto elementwise = [&](auto diag_c) {
+          constexpr bool DIAG = decltype(diag_c)::value;
 #pragma unroll
-        for (int kg = 0; kg < 2; ++kg) {
-          const int key = k_lo + 16 * kg + (lane & 15);
+          for (int kg = 0; kg < 2; ++kg) {
+            const int key = k_lo + 16 * kg + (lane & 15);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            uint32_t hh = 0;  // queries q and q^16 (fl = 0, 1) share one dropout hash
-            if (thr) hh = drop_hash(s32, ((uint32_t)bh * T + q0 + 32 * hq + 4 * g + r) * (uint32_t)T + key);
+            for (int r = 0; r < 4; ++r) {
+              uint32_t hh = 0;  // queries q and q^16 (fl = 0, 1) share one dropout hash
+              if constexpr (DROP) hh = drop_hash(s32, ((uint32_t)bh * T + q0 + 32 * hq + 4 * g + r) * (uint32_t)T + key);
 #pragma unroll
-            for (int fl = 0; fl < 2; ++fl) {
-              float p = exp2f(fmaf(s[kg][fl][r], sl2, -l4[fl][r]));
-              if (diag && q0 + 16 * (2 * hq + fl) + 4 * g + r < key) p = 0.f;
-              float pdv = p, d = dp[kg][fl][r];
-              if (thr) {
-                const bool keep = drop_keep16(hh, fl, thr);
-                pdv = keep ? p * inv_keep : 0.f;
-                d = keep ? d * inv_keep : 0.f;
+              for (int fl = 0; fl < 2; ++fl) {
+                float p = __builtin_amdgcn_exp2f(fmaf(s[kg][fl][r], sl2, -l4[fl][r]));
+                if constexpr (DIAG) p = (q0 + 16 * (2 * hq + fl) + 4 * g + r < key) ? 0.f : p;
+                float pdv = p, d = dp[kg][fl][r];
+                if constexpr (DROP) {
+                  const bool keep = drop_keep16(hh, fl, thr);
+                  pdv = keep ? p : 0.f;
+                  d = keep ? d : 0.f;
+                }
+                dp[kg][fl][r] = pdv;                 // dropped P (for dV)
+                s[kg][fl][r] = p * (d - d4[fl][r]);  // dS
               }
-              dp[kg][fl][r] = pdv;                 // dropped P (for dV)
-              s[kg][fl][r] = p * (d - d4[fl][r]);  // dS
             }
           }
-        }
+        };
+        if (diag) elementwise(std::true_type{});
+        else elementwise(std::false_type{});
         const bf16x8 p0 = pack_perm(dp[0], 0), p1 = pack_perm(dp[1], 0);
         const bf16x8 s0 = pack_perm(s[0], 0), s1 = pack_perm(s[1], 0);
 #pragma unroll
@@ -520,8 +565,10 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dkdv_kernel(const bf16* 
       *reinterpret_cast<bf16x4*>(kout + 16 * fd + 4 * g) =
           bf16x4{f2bf(dk[kg][fd][0] * scale), f2bf(dk[kg][fd][1] * scale), f2bf(dk[kg][fd][2] * scale),
                  f2bf(dk[kg][fd][3] * scale)};
+      const float vs = DROP ? inv_keep : 1.f;
       *reinterpret_cast<bf16x4*>(vout + 16 * fd + 4 * g) =
-          bf16x4{f2bf(dv[kg][fd][0]), f2bf(dv[kg][fd][1]), f2bf(dv[kg][fd][2]), f2bf(dv[kg][fd][3])};
+          bf16x4{f2bf(dv[kg][fd][0] * vs), f2bf(dv[kg][fd][1] * vs), f2bf(dv[kg][fd][2] * vs),
+                 f2bf(dv[kg][fd][3] * vs)};
     }
   }
 }
@@ -552,11 +599,21 @@ GPT2MI_EXPORT int gpt2mi_attn_bwd(const uint16_t* qkv, const uint16_t* out, cons
   attn_delta_kernel<<<(B * T * H + 255) / 256, 256, 0, s>>>((const bf16*)out, (const bf16*)dout, delta, B, T, H);
   int rc = gpt2mi::check_launch("attn_delta");
   if (rc) return rc;
-  attn_bwd_dkdv_kernel<<<dim3((T + BKB - 1) / BKB, B * H), kThreads, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta,
-                                                                 (bf16*)dqkv, T, H, scale, seed, thr, ik);
+  const dim3 gkv((T + BKB - 1) / BKB, B * H);
+  if (thr)
+    attn_bwd_dkdv_kernel<true><<<gkv, kThreads, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta,
+                                                        (bf16*)dqkv, T, H, scale, seed, thr, ik);
+  else
+    attn_bwd_dkdv_kernel<false><<<gkv, kThreads, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta,
+                                                         (bf16*)dqkv, T, H, scale, seed, thr, ik);
   rc = gpt2mi::check_launch("attn_bwd_dkdv");
   if (rc) return rc;
-  attn_bwd_dq_kernel<<<dim3((T + BQ - 1) / BQ, B * H), kThreads, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta,
-                                                              (bf16*)dqkv, T, H, scale, seed, thr, ik);
+  const dim3 gq((T + BQ - 1) / BQ, B * H);
+  if (thr)
+    attn_bwd_dq_kernel<true><<<gq, kThreads, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta, (bf16*)dqkv, T,
+                                                     H, scale, seed, thr, ik);
+  else
+    attn_bwd_dq_kernel<false><<<gq, kThreads, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta, (bf16*)dqkv, T,
+                                                      H, scale, seed, thr, ik);
   return gpt2mi::check_launch("attn_bwd_dq");
 }

@@ -55,12 +55,12 @@ __device__ __forceinline__ float wave_max(float v) {
 // All element / pair indices fit in 32 bits for every BASELINE config (attention B*H*T*T < 2^32).
 __device__ __forceinline__ uint32_t seed32(uint64_t seed) { return (uint32_t)seed ^ (uint32_t)(seed >> 32); }
 __device__ __forceinline__ uint32_t drop_hash(uint32_t s32, uint32_t x) {
-  uint32_t h = x * 0x9E3779B1u + s32;
-  h ^= h >> 15;
-  h *= 0x2C1B3C6Du;
-  h ^= h >> 12;
-  h *= 0x297A2D39u;
-  h ^= h >> 15;
+  // two rounds of multiply-xorshift (murmur3 fmix32 without its last multiply): v_mul_lo_u32 issues
+  // at a quarter of the VALU rate and the hash runs once per element pair in every dropout site
+  uint32_t h = (x ^ s32) * 0x9E3779B1u;
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
   return h;
 }
 __device__ __forceinline__ bool drop_keep16(uint32_t h, int half, uint32_t thr) {
