@@ -289,8 +289,8 @@ GPT2MI_EXPORT int gpt2mi_gemm_wgrad(int M, int N, int K, const uint16_t* A, int 
   splits = (K + P.k_per_split - 1) / P.k_per_split;
   if (splits == 1) {
     P.C = C;
-    if (g_gemm_impl == 0) {
-      const int rc = gpt2mi::gemm_pp_dispatch(2, EPI_F32, P, s, 1);
+    if (g_gemm_impl == 0 || g_gemm_impl >= 3) {
+      const int rc = gpt2mi::gemm_pp_dispatch(2, EPI_F32, P, s, 1, g_gemm_impl >= 3 ? g_gemm_impl - 2 : 0);
       if (rc >= 0) return rc;
     }
     return gpt2mi::gemm256_dispatch(2, EPI_F32, P, s, 1);

@@ -91,13 +91,15 @@ __device__ __forceinline__ bf16x8 frag(const char* slot, int ir0, int kk, int la
     const int ir = ir0 + (lane & 15), c = 4 * kk + (lane >> 4);
     return *reinterpret_cast<const bf16x8*>(slot + ir * 128 + 16 * (c ^ (ir & 7)));
   } else {
+    // k-rows k1 = 32kk + 8g + q and k1 + 4 share one swizzle (mc_swz ignores bits 2 and 5 of k), and
+    // ir0 is a multiple of 16, so the lane part of the address is one VGPR per 16-row fragment
+    // (the kk / hi offsets are immediates): keeps the wgrad (both operands transposed) under 256 VGPRs
     const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
-    const int k1 = 32 * kk + 8 * g + q;
-    const int chunk = (ir0 >> 3) + (p >> 1);
-    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (lds_s16x4*)(slot + k1 * 256 + 16 * ((chunk ^ mc_swz(k1)) & 15) + 8 * (p & 1)));
-    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (lds_s16x4*)(slot + (k1 + 4) * 256 + 16 * ((chunk ^ mc_swz(k1 + 4)) & 15) + 8 * (p & 1)));
+    const int kl = 8 * g + q;
+    const int phys = (((ir0 >> 3) + (p >> 1)) ^ mc_swz(kl)) & 15;
+    const char* a0 = slot + kl * 256 + 16 * phys + 8 * (p & 1) + kk * (32 * 256);
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a0);
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 4 * 256));
     typedef short s16x8 __attribute__((ext_vector_type(8)));
     s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     return __builtin_bit_cast(bf16x8, r);
@@ -329,10 +331,15 @@ namespace gpt2mi {
 // Returns -1 when this kernel does not apply (the caller falls back).
 int gemm_pp_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t s, int splits, int map) {
   if (P.N % BN != 0 || P.k_per_split % (2 * BK) != 0 || P.K % (2 * BK) != 0) return -1;
-  // measured slower than the 2-stage gemm256 kernel (tools/gemm_probe.py): the wgrad instantiations
-  // spill at 256 VGPRs, and the GELU-backward epilogue is bound by its aux-load latency
-  if (map == 0 && layout == 2) return -1;
   if (layout == 2 && P.M % BM != 0) return -1;
+  // wgrad (both operands m-contiguous) stays on the 2-stage gemm256 kernel by default: measured
+  // 698-721 TF vs 765 TF on the lm_head wgrad, 756 vs 852 on qkv (tools/gemm_probe.py, every map)
+  if (map == 0 && layout == 2) return -1;
+  if (map > 0 && layout == 2 && epilogue == EPI_F32) {  // (map - 1) = A/B interleave bits
+    if (map == 1) return launch<true, true, EPI_F32, 0>(P, s, 1);
+    if (map == 2) return launch<true, true, EPI_F32, 1>(P, s, 1);
+    if (map == 3) return launch<true, true, EPI_F32, 2>(P, s, 1);
+  }
   if (map > 0 && epilogue == EPI_BF16 && layout <= 1) {  // half-tile map experiments (tools/gemm_probe.py)
     if (layout == 0) {
       if (map == 1) return launch<false, false, EPI_BF16, 1>(P, s, 1);
