@@ -98,6 +98,23 @@ __device__ __forceinline__ void tile_store(char* base, const u32x4* r) {
   }
 }
 
+// XCD-aware block -> (head, query/key block) map. A 2-D grid dispatches block L = y*gx + x to XCD
+// L % 8, so the plain (x = block, y = head) map puts the 8 blocks of one head on 8 different XCDs
+// (8 private L2s each fetching that head's K/V or Q/dO). Here the blocks that share an XCD take
+// consecutive blocks of ONE head, which then run together out of that XCD's L2.
+__device__ __forceinline__ void attn_block(int& bh, int& blk) {
+  const int nb = gridDim.x, BH = gridDim.y;
+  const int L = blockIdx.y * nb + blockIdx.x;
+  if (BH % 8 == 0) {
+    const int j = L >> 3;
+    bh = (j / nb) * 8 + (L & 7);
+    blk = j % nb;
+  } else {
+    bh = blockIdx.y;
+    blk = blockIdx.x;
+  }
+}
+
 // Dropout of attention probability (q, key) of head bh: 16-bit half (q >> 4) & 1 of
 // drop_hash(seed, (bh*T + (q & ~16))*T + key) — queries q and q^16 of one key share a hash.
 
@@ -108,8 +125,10 @@ __global__ __launch_bounds__(kThreads, 3) void attn_fwd_kernel(const bf16* __res
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * BKV * 128];  // 2 stages x (K, V)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
   const int nqb = (T + BQ - 1) / BQ;
-  const int qb = nqb - 1 - blockIdx.x;  // heavy (late) query blocks first
-  const int bh = blockIdx.y, b = bh / H, h = bh % H;
+  int bh, blk;
+  attn_block(bh, blk);
+  const int qb = nqb - 1 - blk;  // heavy (late) query blocks first
+  const int b = bh / H, h = bh % H;
   const int C = H * D;
   const size_t ld = 3 * (size_t)C;
   const bf16* base = qkv + (size_t)b * T * ld;
@@ -281,8 +300,10 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const bf16* __
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * BKV * 128];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
   const int nqb = (T + BQ - 1) / BQ;
-  const int qb = nqb - 1 - blockIdx.x;
-  const int bh = blockIdx.y, b = bh / H, h = bh % H;
+  int bh, blk;
+  attn_block(bh, blk);
+  const int qb = nqb - 1 - blk;
+  const int b = bh / H, h = bh % H;
   const int C = H * D;
   const size_t ld = 3 * (size_t)C;
   const bf16* base = qkv + (size_t)b * T * ld;
@@ -418,8 +439,9 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dkdv_kernel(const bf16* 
   __shared__ __attribute__((aligned(16))) char smem[2 * kStage];  // 2 x (Q, dO, lse, delta)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
   const int nqt = T / BQT;
-  const int kb = blockIdx.x;  // key block (heaviest first)
-  const int bh = blockIdx.y, b = bh / H, h = bh % H;
+  int bh, kb;  // kb: key block (heaviest first)
+  attn_block(bh, kb);
+  const int b = bh / H, h = bh % H;
   const int C = H * D;
   const size_t ld = 3 * (size_t)C;
   const bf16* base = qkv + (size_t)b * T * ld;

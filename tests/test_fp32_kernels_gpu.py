@@ -93,7 +93,7 @@ def test_gemm_f32_dropout_mask_matches_bf16_kernel():
     assert abs(frac - p) < 0.02
 
 
-@pytest.mark.parametrize("B,T,H", [(1, 64, 1), (2, 256, 3), (1, 1024, 2)])
+@pytest.mark.parametrize("B,T,H", [(1, 64, 1), (2, 256, 3), (1, 1024, 2), (2, 128, 4)])
 def test_attention_f32_fwd_bwd(B, T, H):
     D, C = 64, 64 * H
     g = torch.Generator().manual_seed(B * T + H)
