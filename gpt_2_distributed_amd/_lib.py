@@ -154,11 +154,25 @@ def gemm_wgrad(M, N, K, A, lda, B, ldb, C, ldc, accumulate=True, alpha=1.0, alph
 
 
 def wgrad_splits(M, N, K, cus=256):
-    """Split-K factor for a wgrad output of M x N (K tokens) on 256x256 tiles: fill one wave of the
-    256 CUs, at least 4 K-tiles (of 64) per split."""
+    """Split-K factor for a wgrad output of M x N (K tokens) on 256x256 tiles (one block per CU).
+
+    Minimises (rounds of `cus` blocks) x (K per split) + the slab reduction, so the last round of
+    blocks is not mostly idle: the tied lm_head wgrad (197 x 3 = 591 tiles = 2.3 rounds) runs as 3
+    splits (1773 blocks = 6.9 rounds of 1/3 the depth); the small block wgrads fill one round.
+    Each split keeps >= 4 K-tiles of 64."""
     tiles = (M // 256) * (N // 256)
-    s = 1 if tiles >= cus else max(1, cus // tiles)
-    return max(1, min(s, K // 256))
+    if tiles == 0:
+        return 1
+    best, best_cost = 1, None
+    for s in range(1, 33):
+        if K // s < 256:
+            break
+        rounds = -(-tiles * s // cus)
+        # GEMM time ~ rounds * K/s * 22 ns per token-row of a 256x256 tile; reduce ~ s*M*N*8 B at 5 TB/s
+        cost = rounds * (K / s) * 22e-9 + (s * M * N * 8 / 5e12 if s > 1 else 0.0)
+        if best_cost is None or cost < best_cost * 0.99:
+            best, best_cost = s, cost
+    return best
 
 
 def attn_fwd(qkv, out, lse, B, T, H, D, p_drop=0.0, seed=0):

@@ -107,3 +107,16 @@ def test_loader_partitions_by_rank_gloo():
     out = _spawn(_loader_partition)
     assert out[0][:2] == (0, 2) and out[1][:2] == (1, 2)
     assert out[0][2] and out[1][2] and out[0][2] != out[1][2]
+
+
+def test_wgrad_split_choice_balances_the_last_round():
+    """Host-side split-K choice (gpt_2_distributed_amd/_lib.py): the tied lm_head wgrad (591 tiles =
+    2.3 rounds of 256 CUs) is split 3 ways; the block wgrads fill one round; every split keeps >= 4
+    K-tiles."""
+    from gpt_2_distributed_amd._lib import wgrad_splits
+    assert wgrad_splits(50432, 768, 65536) == 3
+    assert wgrad_splits(3072, 768, 65536) * 36 <= 256
+    assert wgrad_splits(768, 768, 65536) * 9 <= 256
+    for m, n, k in [(50432, 768, 4096), (2304, 768, 1024), (768, 768, 512)]:
+        s = wgrad_splits(m, n, k)
+        assert s >= 1 and k // s >= 256
