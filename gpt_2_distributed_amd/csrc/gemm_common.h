@@ -6,8 +6,9 @@ enum Epi : int {
   EPI_BF16 = 0,      // C_bf16 = alpha*acc (+bias)
   EPI_F32 = 1,       // C_f32 (+)= alpha*acc (+bias)           (accumulate flag)
   EPI_RESID = 2,     // C_f32 = resid_f32 + drop(alpha*acc + bias)          (proj / fc2 + residual)
-  EPI_GELU = 3,      // aux_bf16 = u = acc+bias ; C_bf16 = drop(gelu_tanh(u))   (fc1 + NewGELU + drop1)
-  EPI_GELU_BWD = 4,  // C_bf16 = drop_mask(alpha*acc) * gelu'(aux_bf16)        (fc2 dgrad -> fc1 output grad)
+  EPI_GELU = 3,      // u = acc+bias: C = drop(gelu_tanh(u)), aux = keep/(1-p) * gelu'(u)  (fc1 + NewGELU + drop1)
+  EPI_GELU_BWD = 4,  // C = alpha*acc * aux          (fc2 dgrad -> fc1 pre-activation grad: mask and gelu'
+                     //                               were folded into aux by the forward epilogue)
   EPI_ATOMIC = 5,    // atomicAdd(C_f32, alpha*acc)            (split-K wgrad into the grad arena)
   EPI_SLAB = 6,      // split-K partial tile -> fp32 slab[blockIdx.y] (gemm256 wgrad; summed by splitk_reduce)
 };
@@ -18,7 +19,7 @@ struct GemmParams {
   void* C;
   const float* bias;
   const float* resid;
-  void* aux;  // EPI_GELU: pre-activation out; EPI_GELU_BWD: pre-activation in (element type = TE)
+  void* aux;  // EPI_GELU: masked GELU derivative out; EPI_GELU_BWD: the same, in (element type = TE)
   const float* alpha_dev;
   int M, N, K, lda, ldb, ldc, ldaux;
   int k_per_split;
@@ -39,11 +40,11 @@ __device__ __forceinline__ float gelu_sig(float u) {
   return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(m2log2e * z));
 }
 __device__ __forceinline__ float gelu_f(float u) { return u * gelu_sig(u); }
-__device__ __forceinline__ float gelu_grad_f(float u) {
+__device__ __forceinline__ float gelu_grad_from_sig(float u, float sg) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  const float sg = gelu_sig(u);
   return sg * (1.f + 2.f * k0 * u * (1.f - sg) * (1.f + 3.f * k1 * u * u));
 }
+__device__ __forceinline__ float gelu_grad_f(float u) { return gelu_grad_from_sig(u, gelu_sig(u)); }
 
 // keep mask of the 4 dropout elements didx..didx+3 (didx even): two hashes, 16 bits per element
 __device__ __forceinline__ void drop4(const GemmParams& P, uint64_t didx, bool keep[4]) {
@@ -96,7 +97,7 @@ __device__ __forceinline__ void epilogue_apply(const GemmParams& P, int gm, int 
   const size_t cidx = (size_t)gm * P.ldc + gn;
   const uint64_t didx = (uint64_t)gm * P.N + gn;  // dropout element index in the logical [M,N] (even)
   bool keep[4] = {true, true, true, true};
-  if (EPI == EPI_RESID || EPI == EPI_GELU || EPI == EPI_GELU_BWD)
+  if (EPI == EPI_RESID || EPI == EPI_GELU)
     if (P.thr) drop4(P, didx, keep);
   if constexpr (EPI == EPI_BF16) {
     store4<TE>(reinterpret_cast<TE*>(P.C) + cidx, v);
@@ -113,24 +114,27 @@ __device__ __forceinline__ void epilogue_apply(const GemmParams& P, int gm, int 
     }
     *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(P.C) + cidx) = opnd;
   } else if constexpr (EPI == EPI_GELU) {
-    f32x4 h;
+    // the forward also emits what the backward needs of this site: dL/du = dL/dh * keep/(1-p) * gelu'(u),
+    // so the fc2 dgrad epilogue is one multiply (no dropout hash, no GELU math, no pre-activation)
+    f32x4 h, dg;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      float a = gelu_f(v[j]);
-      if (P.thr) a = keep[j] ? a * P.inv_keep : 0.f;
+      const float sg = gelu_sig(v[j]);
+      float a = v[j] * sg;
+      float d = gelu_grad_from_sig(v[j], sg);
+      if (P.thr) {
+        a = keep[j] ? a * P.inv_keep : 0.f;
+        d = keep[j] ? d * P.inv_keep : 0.f;
+      }
       h[j] = a;
+      dg[j] = d;
     }
-    store4<TE>(reinterpret_cast<TE*>(P.aux) + (size_t)gm * P.ldaux + gn, v);
+    store4<TE>(reinterpret_cast<TE*>(P.aux) + (size_t)gm * P.ldaux + gn, dg);
     store4<TE>(reinterpret_cast<TE*>(P.C) + cidx, h);
   } else if constexpr (EPI == EPI_GELU_BWD) {
-    // gelu' is evaluated at the STORED pre-activation (bf16-rounded under autocast), as autograd does
     f32x4 o;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float d = v[j];
-      if (P.thr) d = keep[j] ? d * P.inv_keep : 0.f;
-      o[j] = d * gelu_grad_f(opnd[j]);
-    }
+    for (int j = 0; j < 4; ++j) o[j] = v[j] * opnd[j];
     store4<TE>(reinterpret_cast<TE*>(P.C) + cidx, o);
   } else if constexpr (EPI == EPI_ATOMIC) {
     float* C = reinterpret_cast<float*>(P.C);

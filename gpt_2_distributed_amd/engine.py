@@ -12,7 +12,7 @@ counter-based mask that backward regenerates; eval mode / p = 0 disables it.
 HBM layout per (B, T) workspace (M = B*T tokens, C = n_embd, Vp = vocab padded to 128):
   residual stream x[l]          fp32 [L+1][M, C]
   per block: ln1, ln2 bf16 [M,C]; mean/rstd fp32 [M]; qkv bf16 [M,3C]; attn out bf16 [M,C];
-             lse fp32 [B*H,T]; x_mid fp32 [M,C]; fc1 pre-activation u and gelu h bf16 [M,4C]
+             lse fp32 [B*H,T]; x_mid fp32 [M,C]; gelu output h and dgelu = keep/(1-p)*gelu'(u) bf16 [M,4C]
   head:      ln_f bf16 [M,C]; logits bf16 [M,Vp] (returned as a [B,T,V] view); dlogits bf16 [M,Vp]
   backward scratch: dres fp32 [M,C], dres_bf bf16 [M,C], dln bf16 [M,C], dU bf16 [M,4C],
              dqkv bf16 [M,3C], delta fp32 [B*H,T]
@@ -53,7 +53,7 @@ class BlockActs:
     ln2: torch.Tensor
     m2: torch.Tensor
     r2: torch.Tensor
-    u: torch.Tensor
+    dgelu: torch.Tensor  # keep/(1-p) * gelu'(u) of the fc1 pre-activation u (from the fc1 epilogue)
     h: torch.Tensor
 
 
@@ -70,7 +70,7 @@ class Workspace:
             self.blocks.append(BlockActs(
                 ln1=e(M, C), m1=e(M, dt=F32), r1=e(M, dt=F32), qkv=e(M, 3 * C), ao=e(M, C),
                 lse=e(B * H, T, dt=F32), xmid=e(M, C, dt=F32), ln2=e(M, C), m2=e(M, dt=F32), r2=e(M, dt=F32),
-                u=e(M, 4 * C), h=e(M, 4 * C)))
+                dgelu=e(M, 4 * C), h=e(M, 4 * C)))
         self.lnf = e(M, C)
         self.mf = e(M, dt=F32)
         self.rf = e(M, dt=F32)
@@ -334,7 +334,7 @@ class Engine:
                             M, C, cfg.layer_norm_eps)
             with self._probe("fc1_fwd"):
                 K.gemm(K.FWD, K.EPI_GELU, M, 4 * C, C, A.ln2, C, W(pre + "mlp.fc1.weight"), C, A.h, 4 * C,
-                       bias=self.p(pre + "mlp.fc1.bias"), aux=A.u, ldaux=4 * C, p_drop=pr, seed=seeds[("fc1", l)])
+                       bias=self.p(pre + "mlp.fc1.bias"), aux=A.dgelu, ldaux=4 * C, p_drop=pr, seed=seeds[("fc1", l)])
             K.gemm(K.FWD, K.EPI_RESID, M, C, 4 * C, A.h, 4 * C, W(pre + "mlp.fc2.weight"), 4 * C, x[l + 1], C,
                    bias=self.p(pre + "mlp.fc2.bias"), resid=A.xmid, p_drop=pr, seed=seeds[("fc2", l)])
         K.layernorm_fwd(x[L], self.p("transformer.ln_f.weight"), self.p("transformer.ln_f.bias"), ws.lnf, None,
@@ -403,7 +403,7 @@ class Engine:
             pre = f"transformer.h.{l}."
             # ---- MLP: dY2 = dres_bf (fc2 dropout applied), db2 done by the LN bwd above
             K.gemm(K.DGRAD, K.EPI_GELU_BWD, M, 4 * C, C, ws.dres_bf, C, W(pre + "mlp.fc2.weight"), 4 * C,
-                   ws.dU, 4 * C, aux=A.u, ldaux=4 * C, p_drop=pr, seed=seeds[("fc1", l)])
+                   ws.dU, 4 * C, aux=A.dgelu, ldaux=4 * C)
             wgrad(C, 4 * C, ws.dres_bf, C, A.h, 4 * C, self.g(pre + "mlp.fc2.weight"))
             K.gemm(K.DGRAD, K.EPI_BF16, M, C, 4 * C, ws.dU, 4 * C, W(pre + "mlp.fc1.weight"), C, ws.dln, C)
             wgrad(4 * C, C, ws.dU, 4 * C, A.ln2, C, self.g(pre + "mlp.fc1.weight"))

@@ -55,8 +55,9 @@ int gpt2mi_colsum_bf16(const uint16_t* g, float* db, int M, int N, int ld, void*
  * layout 0: A[M][K], B[N][K]   (x @ W^T)        layout 1: A[M][K], B[K][N]   (dY @ W, dgrad)
  * layout 2: A[K][M], B[K][N]   (dY^T @ X, wgrad)
  * epilogue 0 BF16: C bf16 (+bias)            1 F32: C fp32 (+bias), += when accumulate
- *          2 RESID: C fp32 = resid + drop(acc+bias)       3 GELU: aux = bf16(acc+bias), C = bf16(drop(gelu))
- *          4 GELU_BWD: C = bf16(drop(acc) * gelu'(aux))    5 ATOMIC: C fp32 += acc (split-K over `splits`)
+ *          2 RESID: C fp32 = resid + drop(acc+bias)
+ *          3 GELU: u = acc+bias, C = bf16(drop(gelu(u))), aux = bf16(keep/(1-p) * gelu'(u)) (what backward needs)
+ *          4 GELU_BWD: C = bf16(acc * aux) (aux from the GELU forward)   5 ATOMIC: C fp32 += acc (split-K)
  * Requires M, N multiples of 128 and K a multiple of 64*splits. */
 int gpt2mi_gemm(int layout, int epilogue, int M, int N, int K, const uint16_t* A, int lda, const uint16_t* B, int ldb,
                 void* C, int ldc, const float* bias, const float* resid, uint16_t* aux, int ldaux, float alpha,

@@ -65,18 +65,16 @@ def test_gemm_f32_epilogues():
     Cr = torch.empty(M, N, device=dev)
     L().gemm(0, L().EPI_RESID, M, N, K, Ad, K, Wd, K, Cr, N, bias=bias.to(dev), resid=resid.to(dev))
     assert rel_err(Cr.cpu(), resid.double() + acc + bias.double()) < 2e-6
-    Cg, U = torch.empty(M, N, device=dev), torch.empty(M, N, device=dev)
-    L().gemm(0, L().EPI_GELU, M, N, K, Ad, K, Wd, K, Cg, N, bias=bias.to(dev), aux=U, ldaux=N)
-    u = acc + bias.double()
-    assert rel_err(U.cpu(), u) < 2e-6
-    assert rel_err(Cg.cpu(), model_ref.gelu_tanh(u)) < 1e-5
-    # GELU backward through the fc2 dgrad: dU = (dY @ W2) * gelu'(U)
+    Cg, G = torch.empty(M, N, device=dev), torch.empty(M, N, device=dev)
+    L().gemm(0, L().EPI_GELU, M, N, K, Ad, K, Wd, K, Cg, N, bias=bias.to(dev), aux=G, ldaux=N)
+    u = (acc + bias.double()).requires_grad_(True)
+    assert rel_err(Cg.cpu(), model_ref.gelu_tanh(u.detach())) < 1e-5
+    # GELU backward through the fc2 dgrad: dU = (dY @ W2) * gelu'(u), gelu'(u) emitted by the forward
     dY, W2 = torch.randn(M, K, generator=g), torch.randn(K, N, generator=g) * 0.05
     dU = torch.empty(M, N, device=dev)
-    L().gemm(1, L().EPI_GELU_BWD, M, N, K, dY.to(dev), K, W2.to(dev), N, dU, N, aux=U, ldaux=N)
-    uu = U.cpu().double().requires_grad_(True)
-    model_ref.gelu_tanh(uu).backward(_ref(1, dY, W2))
-    assert rel_err(dU.cpu(), uu.grad) < 1e-5
+    L().gemm(1, L().EPI_GELU_BWD, M, N, K, dY.to(dev), K, W2.to(dev), N, dU, N, aux=G, ldaux=N)
+    model_ref.gelu_tanh(u).backward(_ref(1, dY, W2))
+    assert rel_err(dU.cpu(), u.grad) < 1e-5
 
 
 def test_gemm_f32_dropout_mask_matches_bf16_kernel():

@@ -171,25 +171,34 @@ def test_gemm_epilogues_forward():
     Cr = torch.empty(M, N, device=dev)
     L().gemm(0, L().EPI_RESID, M, N, K, Ad, K, Wd, K, Cr, N, bias=bias.to(dev), resid=resid.to(dev))
     assert rel_err(Cr.cpu(), resid + acc + bias) < 1e-5
-    # GELU: aux = pre-activation, C = gelu
+    # GELU: C = gelu(u), aux = gelu'(u) (no dropout: keep = 1)
     Cg = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
-    U = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
-    L().gemm(0, L().EPI_GELU, M, N, K, Ad, K, Wd, K, Cg, N, bias=bias.to(dev), aux=U, ldaux=N)
-    u = acc + bias
-    assert rel_err(U.cpu().float(), u) < 4e-3
-    assert rel_err(Cg.cpu().float(), model_ref.gelu_tanh(u)) < 4e-3
+    G = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    L().gemm(0, L().EPI_GELU, M, N, K, Ad, K, Wd, K, Cg, N, bias=bias.to(dev), aux=G, ldaux=N)
+    u = (acc + bias).requires_grad_(True)
+    model_ref.gelu_tanh(u).sum().backward()
+    assert rel_err(G.cpu().float(), u.grad) < 4e-3
+    assert rel_err(Cg.cpu().float(), model_ref.gelu_tanh(u.detach())) < 4e-3
 
 
 def test_gemm_gelu_bwd_dgrad():
-    M, N, K = 256, 256, 384  # dH[M,N] = dY[M,K] @ W2[K,N]; dU = dH * gelu'(U)
+    """fc1 forward (EPI_GELU, with dropout) then fc2 dgrad (EPI_GELU_BWD) reproduce autograd of
+    drop(gelu(u)): dU = (dY @ W2) * keep/(1-p) * gelu'(u), with the mask regenerated nowhere."""
+    M, N, K = 256, 256, 384  # u[M,N] = X[M,K'] W1^T ; dH[M,N] = dY[M,K] @ W2[K,N]
     g = torch.Generator().manual_seed(4)
+    X, W1 = bf(torch.randn(M, 128, generator=g)), bf(torch.randn(N, 128, generator=g) * 0.1)
     dY, W2 = bf(torch.randn(M, K, generator=g)), bf(torch.randn(K, N, generator=g) * 0.05)
-    U = bf(torch.randn(M, N, generator=g))
+    p = 0.25
+    H = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    G = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    L().gemm(0, L().EPI_GELU, M, N, 128, X.to(dev), 128, W1.to(dev), 128, H, N, aux=G, ldaux=N, p_drop=p, seed=9)
     C = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
-    L().gemm(1, L().EPI_GELU_BWD, M, N, K, dY.to(dev), K, W2.to(dev), N, C, N, aux=U.to(dev), ldaux=N)
-    u = U.float().requires_grad_(True)
-    model_ref.gelu_tanh(u).backward(dY.float() @ W2.float())
-    assert rel_err(C.cpu().float(), u.grad) < 5e-3
+    L().gemm(1, L().EPI_GELU_BWD, M, N, K, dY.to(dev), K, W2.to(dev), N, C, N, aux=G, ldaux=N)
+    keep = (H.cpu().float() != 0).float()  # gelu(u) != 0 almost surely: the kept set
+    assert abs(1 - keep.mean().item() - p) < 0.03
+    u = (X.float() @ W1.float().t()).requires_grad_(True)
+    (model_ref.gelu_tanh(u) * keep / (1 - p)).backward(dY.float() @ W2.float())
+    assert rel_err(C.cpu().float(), u.grad) < 1e-2
 
 
 def test_gemm_rejects_bad_shapes():

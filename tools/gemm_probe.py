@@ -88,5 +88,33 @@ def main():
         print(line, flush=True)
 
 
+
+
+def hipblaslt_reference():
+    """torch.matmul (hipBLASLt) on the lm_head shapes, same random data style (reference points only)."""
+    r = lambda *s: (torch.rand(*s, device=dev) * 2 - 1).to(torch.bfloat16)  # noqa: E731
+    cases = {
+        "lm_fwd": (lambda a, b: a @ b.t(), r(65536, 768), r(50432, 768)),
+        "lm_dgrad": (lambda a, b: a @ b, r(65536, 50432), r(50432, 768)),
+        "lm_wgrad": (lambda a, b: a.t() @ b, r(65536, 50432), r(65536, 768)),
+    }
+    for name, (f, a, b) in cases.items():
+        f(a, b)
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(5):
+            f(a, b)
+        e.record()
+        torch.cuda.synchronize()
+        ms = s.elapsed_time(e) / 5
+        print(f"[hipBLASLt] {name}: {ms:.3f} ms {2 * 65536 * 50432 * 768 / ms / 1e9:.0f} TF", flush=True)
+        del a, b
+
+
 if __name__ == "__main__":
-    main()
+    if "blaslt" in sys.argv[1:]:
+        K.load()
+        hipblaslt_reference()
+    else:
+        main()
