@@ -27,7 +27,7 @@ _SIGS = {
     "gpt2mi_layernorm_bwd": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_float, _c_u64, _c_int, _p],
     "gpt2mi_colsum_bf16": [_p, _p, _c_int, _c_int, _c_int, _p],
     "gpt2mi_gemm": [_c_int, _c_int, _c_int, _c_int, _c_int, _p, _c_int, _p, _c_int, _p, _c_int, _p, _p, _p, _c_int,
-                    _c_float, _p, _c_int, _c_int, _c_float, _c_u64, _p],
+                    _c_float, _p, _c_int, _c_int, _c_float, _c_u64, _p, _p],
     "gpt2mi_attn_fwd": [_p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_float, _c_u64, _p],
     "gpt2mi_attn_bwd": [_p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_float, _c_u64, _p],
     "gpt2mi_xent_fwd": [_p, _c_int, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _p, _p, _p],
@@ -40,7 +40,7 @@ _SIGS = {
     "gpt2mi_memset_zero": [_p, _c_size, _p],
     "gpt2mi_set_gemm_impl": [_c_int],
     "gpt2mi_gemm_f32": [_c_int, _c_int, _c_int, _c_int, _c_int, _p, _c_int, _p, _c_int, _p, _c_int, _p, _p, _p,
-                        _c_int, _c_float, _p, _c_int, _c_int, _c_float, _c_u64, _p],
+                        _c_int, _c_float, _p, _c_int, _c_int, _c_float, _c_u64, _p, _p],
     "gpt2mi_attn_fwd_f32": [_p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_float, _c_u64, _p],
     "gpt2mi_attn_bwd_f32": [_p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_float, _c_u64, _p],
     "gpt2mi_layernorm_bwd_f32": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_float, _c_u64, _c_int,
@@ -141,9 +141,10 @@ def colsum_bf16(g, db, M, N, ld):
 
 
 def gemm(layout, epilogue, M, N, K, A, lda, B, ldb, C, ldc, bias=None, resid=None, aux=None, ldaux=0,
-         alpha=1.0, alpha_dev=None, accumulate=False, splits=1, p_drop=0.0, seed=0):
+         alpha=1.0, alpha_dev=None, accumulate=False, splits=1, p_drop=0.0, seed=0, dbias=None):
     _call("gpt2mi_gemm_f32" if _f32(A) else "gpt2mi_gemm", layout, epilogue, M, N, K, _ptr(A), lda, _ptr(B), ldb, _ptr(C), ldc, _ptr(bias),
-          _ptr(resid), _ptr(aux), ldaux, alpha, _ptr(alpha_dev), int(accumulate), splits, p_drop, seed, _stream())
+          _ptr(resid), _ptr(aux), ldaux, alpha, _ptr(alpha_dev), int(accumulate), splits, p_drop, seed, _ptr(dbias),
+          _stream())
 
 
 def gemm_wgrad(M, N, K, A, lda, B, ldb, C, ldc, accumulate=True, alpha=1.0, alpha_dev=None, workspace=None,

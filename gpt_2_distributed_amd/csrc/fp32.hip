@@ -16,6 +16,7 @@
 //    drop the same probabilities.
 #include "common.h"
 #include "gemm_common.h"
+#include "gpt2mi.h"
 
 namespace {
 
@@ -373,7 +374,15 @@ __global__ __launch_bounds__(kAThreads) void attn_bwd_dq_f32_kernel(
 GPT2MI_EXPORT int gpt2mi_gemm_f32(int layout, int epilogue, int M, int N, int K, const float* A, int lda, const float* B,
                                   int ldb, void* C, int ldc, const float* bias, const float* resid, float* aux,
                                   int ldaux, float alpha, const float* alpha_dev, int accumulate, int splits,
-                                  float p_drop, uint64_t seed, void* stream) {
+                                  float p_drop, uint64_t seed, float* dbias, void* stream) {
+  GPT2MI_REQUIRE(dbias == nullptr || ((epilogue == EPI_BF16 || epilogue == EPI_GELU_BWD) && layout <= 1),
+                 "gemm_f32: dbias (fused column sum) needs the BF16 or GELU_BWD epilogue of layout 0/1");
+  if (dbias) {
+    const int rc = gpt2mi_gemm_f32(layout, epilogue, M, N, K, A, lda, B, ldb, C, ldc, bias, resid, aux, ldaux, alpha,
+                                   alpha_dev, accumulate, splits, p_drop, seed, nullptr, stream);
+    if (rc) return rc;
+    return gpt2mi_colsum_f32((const float*)C, dbias, M, N, ldc, stream);
+  }
   GPT2MI_REQUIRE(M > 0 && N >= 4 && N % 4 == 0 && K % FBK == 0, "gemm_f32: need N=%d %% 4 == 0 and K=%d %% 16 == 0",
                  N, K);
   GPT2MI_REQUIRE(layout >= 0 && layout <= 2, "gemm_f32: bad layout %d", layout);

@@ -19,6 +19,7 @@
 // Epilogue: accumulators -> LDS (fp32, padded rows) -> row-contiguous 16-B chunks -> fused op -> HBM.
 #include "common.h"
 #include "gemm_common.h"
+#include "gpt2mi.h"
 
 namespace {
 
@@ -216,7 +217,9 @@ GPT2MI_EXPORT void gpt2mi_set_gemm_impl(int impl) { g_gemm_impl = impl; }
 GPT2MI_EXPORT int gpt2mi_gemm(int layout, int epilogue, int M, int N, int K, const uint16_t* A, int lda,
                               const uint16_t* B, int ldb, void* C, int ldc, const float* bias, const float* resid,
                               uint16_t* aux, int ldaux, float alpha, const float* alpha_dev, int accumulate,
-                              int splits, float p_drop, uint64_t seed, void* stream) {
+                              int splits, float p_drop, uint64_t seed, float* dbias, void* stream) {
+  GPT2MI_REQUIRE(dbias == nullptr || ((epilogue == EPI_BF16 || epilogue == EPI_GELU_BWD) && layout <= 1),
+                 "gemm: dbias (fused column sum) needs the BF16 or GELU_BWD epilogue of layout 0/1");
   GPT2MI_REQUIRE(N % BN == 0 && M % 64 == 0 && M > 0, "gemm: N=%d must be a multiple of %d and M=%d of 64", N, BN, M);
   GPT2MI_REQUIRE(layout != 2 || M % BM == 0, "gemm: wgrad needs M=%d a multiple of %d", M, BM);
   GPT2MI_REQUIRE(splits >= 1 && K % (BK * splits) == 0, "gemm: K=%d must be a multiple of %d*splits(%d)", K, BK,
@@ -232,6 +235,7 @@ GPT2MI_EXPORT int gpt2mi_gemm(int layout, int epilogue, int M, int N, int K, con
   P.resid = resid;
   P.aux = aux;
   P.alpha_dev = alpha_dev;
+  P.dbias = dbias;
   P.M = M; P.N = N; P.K = K;
   P.lda = lda; P.ldb = ldb; P.ldc = ldc; P.ldaux = ldaux;
   P.k_per_split = K / splits;
@@ -244,7 +248,14 @@ GPT2MI_EXPORT int gpt2mi_gemm(int layout, int epilogue, int M, int N, int K, con
   const bool big_ok = splits == 1 && N % 256 == 0 && epilogue != EPI_ATOMIC && (layout <= 1 || M % 256 == 0);
   if (big_ok && (g_gemm_impl == 0 || g_gemm_impl >= 3)) {
     const int rc = gpt2mi::gemm_pp_dispatch(layout, epilogue, P, s, 1, g_gemm_impl >= 3 ? g_gemm_impl - 2 : 0);
-    if (rc >= 0) return rc;
+    if (rc >= 0) return rc;  // the ping-pong kernel fuses dbias
+  }
+  if (dbias) {  // other kernels: the GEMM, then the column sums of its output
+    P.dbias = nullptr;
+    const int rc = gpt2mi_gemm(layout, epilogue, M, N, K, A, lda, B, ldb, C, ldc, bias, resid, aux, ldaux, alpha,
+                               alpha_dev, accumulate, splits, p_drop, seed, nullptr, stream);
+    if (rc) return rc;
+    return gpt2mi_colsum_bf16((const uint16_t*)C, dbias, M, N, ldc, stream);
   }
   if (big_ok && g_gemm_impl != 1) {
     const int rc = gpt2mi::gemm256_dispatch(layout, epilogue, P, s, 1);

@@ -21,6 +21,7 @@ struct GemmParams {
   const float* resid;
   void* aux;  // EPI_GELU: masked GELU derivative out; EPI_GELU_BWD: the same, in (element type = TE)
   const float* alpha_dev;
+  float* dbias;  // optional: dbias[n] += sum_m C[m][n] of the stored output (bias grad of the next op)
   int M, N, K, lda, ldb, ldc, ldaux;
   int k_per_split;
   float alpha;
@@ -63,6 +64,15 @@ __device__ __forceinline__ void store4(TE* p, f32x4 v) {
   if constexpr (sizeof(TE) == 2) *reinterpret_cast<bf16x4*>(p) = bf16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
   else *reinterpret_cast<f32x4*>(p) = v;
 }
+// v as stored in TE (bf16 rounding)
+template <typename TE>
+__device__ __forceinline__ f32x4 round4(f32x4 v) {
+  if constexpr (sizeof(TE) == 2) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = bf2f(f2bf(v[j]));
+  }
+  return v;
+}
 template <typename TE>
 __device__ __forceinline__ f32x4 load4(const TE* p) {
   if constexpr (sizeof(TE) == 2) {
@@ -92,8 +102,9 @@ __device__ __forceinline__ f32x4 epilogue_operand(const GemmParams& P, int gm, i
 
 // Apply the fused epilogue to 4 consecutive outputs C[gm][gn..gn+3]; v = alpha*acc (+bias), opnd =
 // epilogue_operand(gm, gn). TE = element type of the bf16-or-fp32 outputs (C of BF16/GELU/GELU_BWD, aux).
+// Returns the primary output as stored for BF16 / GELU_BWD (for fused column sums), v otherwise.
 template <int EPI, typename TE = bf16>
-__device__ __forceinline__ void epilogue_apply(const GemmParams& P, int gm, int gn, f32x4 v, f32x4 opnd) {
+__device__ __forceinline__ f32x4 epilogue_apply(const GemmParams& P, int gm, int gn, f32x4 v, f32x4 opnd) {
   const size_t cidx = (size_t)gm * P.ldc + gn;
   const uint64_t didx = (uint64_t)gm * P.N + gn;  // dropout element index in the logical [M,N] (even)
   bool keep[4] = {true, true, true, true};
@@ -101,6 +112,7 @@ __device__ __forceinline__ void epilogue_apply(const GemmParams& P, int gm, int 
     if (P.thr) drop4(P, didx, keep);
   if constexpr (EPI == EPI_BF16) {
     store4<TE>(reinterpret_cast<TE*>(P.C) + cidx, v);
+    return round4<TE>(v);
   } else if constexpr (EPI == EPI_F32) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) v[j] += opnd[j];
@@ -136,11 +148,13 @@ __device__ __forceinline__ void epilogue_apply(const GemmParams& P, int gm, int 
 #pragma unroll
     for (int j = 0; j < 4; ++j) o[j] = v[j] * opnd[j];
     store4<TE>(reinterpret_cast<TE*>(P.C) + cidx, o);
+    return round4<TE>(o);
   } else if constexpr (EPI == EPI_ATOMIC) {
     float* C = reinterpret_cast<float*>(P.C);
 #pragma unroll
     for (int j = 0; j < 4; ++j) atomicAdd(C + cidx + j, v[j]);
   }
+  return v;
 }
 
 template <int EPI, typename TE = bf16>

@@ -252,6 +252,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   const f32x4 bias = (P.bias && EPI != EPI_GELU_BWD) ? *reinterpret_cast<const f32x4*>(P.bias + gn)
                                                      : f32x4{0.f, 0.f, 0.f, 0.f};
   constexpr bool kOpnd = EPI == EPI_RESID || EPI == EPI_GELU_BWD || EPI == EPI_F32;
+  constexpr bool kCsum = EPI == EPI_BF16 || EPI == EPI_GELU_BWD;  // fused bias grad of the stored output
+  const bool csum_on = kCsum && P.dbias != nullptr;
+  f32x4 csum = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi) {
     // the pass's epilogue operands (residual / pre-activation / old C): all 16 loads in flight
@@ -292,7 +295,13 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
         float* slab = reinterpret_cast<float*>(P.C) + (size_t)blockIdx.y * P.M * P.ldc;
         *reinterpret_cast<f32x4*>(slab + (size_t)gm * P.ldc + gn) = v;
       } else {
-        epilogue_apply<EPI>(P, gm, gn, v, kOpnd ? opnd[it] : f32x4{0.f, 0.f, 0.f, 0.f});
+        const f32x4 o = epilogue_apply<EPI>(P, gm, gn, v, kOpnd ? opnd[it] : f32x4{0.f, 0.f, 0.f, 0.f});
+        if constexpr (kCsum) {
+          if (csum_on) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) csum[e] += o[e];
+          }
+        }
       }
     };
     if (m0 + BM <= P.M) {  // full tile (block-uniform): straight-line reads, then the stores
@@ -309,6 +318,19 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
         const int r = it * 8 + (tid >> 6);
         const f32x4 v = *reinterpret_cast<const f32x4*>(img + r * 256 + 4 * (ch ^ (r & 15)));
         if (row_of(it) < P.M) finish(it, v);
+      }
+    }
+  }
+  if constexpr (kCsum) {
+    if (csum_on) {  // the 8 waves hold partial sums of the same 256 columns: reduce in LDS, 1 atomic/column
+      lds_barrier();  // every wave has finished reading the staging image
+      *reinterpret_cast<f32x4*>(img + (tid >> 6) * 256 + 4 * ch) = csum;
+      lds_barrier();
+      if (tid < 256) {
+        float t = 0.f;
+#pragma unroll
+        for (int w8 = 0; w8 < 8; ++w8) t += img[w8 * 256 + tid];
+        atomicAdd(P.dbias + n0 + tid, t);
       }
     }
   }

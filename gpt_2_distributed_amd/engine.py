@@ -403,11 +403,10 @@ class Engine:
             pre = f"transformer.h.{l}."
             # ---- MLP: dY2 = dres_bf (fc2 dropout applied), db2 done by the LN bwd above
             K.gemm(K.DGRAD, K.EPI_GELU_BWD, M, 4 * C, C, ws.dres_bf, C, W(pre + "mlp.fc2.weight"), 4 * C,
-                   ws.dU, 4 * C, aux=A.dgelu, ldaux=4 * C)
+                   ws.dU, 4 * C, aux=A.dgelu, ldaux=4 * C, dbias=self.g(pre + "mlp.fc1.bias"))
             wgrad(C, 4 * C, ws.dres_bf, C, A.h, 4 * C, self.g(pre + "mlp.fc2.weight"))
             K.gemm(K.DGRAD, K.EPI_BF16, M, C, 4 * C, ws.dU, 4 * C, W(pre + "mlp.fc1.weight"), C, ws.dln, C)
             wgrad(4 * C, C, ws.dU, 4 * C, A.ln2, C, self.g(pre + "mlp.fc1.weight"))
-            K.colsum_bf16(ws.dU, self.g(pre + "mlp.fc1.bias"), M, 4 * C, 4 * C)
             K.layernorm_bwd(A.xmid, self.p(pre + "ln2.weight"), A.m2, A.r2, ws.dln, ws.dres, self.g(pre + "ln2.weight"),
                             self.g(pre + "ln2.bias"), ws.dres_bf, self.g(pre + "attn.proj.bias"), M, C, pr,
                             seeds[("proj", l)])

@@ -58,10 +58,13 @@ int gpt2mi_colsum_bf16(const uint16_t* g, float* db, int M, int N, int ld, void*
  *          2 RESID: C fp32 = resid + drop(acc+bias)
  *          3 GELU: u = acc+bias, C = bf16(drop(gelu(u))), aux = bf16(keep/(1-p) * gelu'(u)) (what backward needs)
  *          4 GELU_BWD: C = bf16(acc * aux) (aux from the GELU forward)   5 ATOMIC: C fp32 += acc (split-K)
+ * dbias (may be NULL; BF16 / GELU_BWD epilogues of layouts 0/1): dbias[n] += sum_m C[m][n] of the stored
+ * output — the bias gradient of the Linear whose output grad C is (fused into the 256x256 epilogue).
  * Requires M, N multiples of 128 and K a multiple of 64*splits. */
 int gpt2mi_gemm(int layout, int epilogue, int M, int N, int K, const uint16_t* A, int lda, const uint16_t* B, int ldb,
                 void* C, int ldc, const float* bias, const float* resid, uint16_t* aux, int ldaux, float alpha,
-                const float* alpha_dev, int accumulate, int splits, float p_drop, uint64_t seed, void* stream);
+                const float* alpha_dev, int accumulate, int splits, float p_drop, uint64_t seed, float* dbias,
+                void* stream);
 
 /* Weight gradient (train_gpt2_distributed.py:412 autograd wgrad of every nn.Linear):
  * C[M][N] (+)= alpha*(alpha_dev?) * A^T B, A stored [K][M] (dY), B stored [K][N] (X), K = tokens.
@@ -103,7 +106,8 @@ int gpt2mi_norm_partials_size(void);
 /* K3/K9-K12/K14 in fp32: N % 4 == 0, K % (16*splits) == 0, leading dims % 4 == 0. */
 int gpt2mi_gemm_f32(int layout, int epilogue, int M, int N, int K, const float* A, int lda, const float* B, int ldb,
                     void* C, int ldc, const float* bias, const float* resid, float* aux, int ldaux, float alpha,
-                    const float* alpha_dev, int accumulate, int splits, float p_drop, uint64_t seed, void* stream);
+                    const float* alpha_dev, int accumulate, int splits, float p_drop, uint64_t seed, float* dbias,
+                    void* stream);
 /* K4-K8 in fp32 (model.py:124-155 without autocast); same dropout mask as gpt2mi_attn_fwd. */
 int gpt2mi_attn_fwd_f32(const float* qkv, float* out, float* lse, int B, int T, int H, int head_dim, float p_drop,
                         uint64_t seed, void* stream);

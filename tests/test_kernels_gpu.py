@@ -404,3 +404,21 @@ def test_gemm_pingpong_vs_fp64(layout, M, N, K):
     L().gemm(layout, L().EPI_F32, M, N, K, A.to(dev), K, B.to(dev), B.shape[1], C, N, alpha=0.25)
     torch.cuda.synchronize()
     assert rel_err(C.cpu(), 0.25 * ref) < 1e-6
+
+
+@pytest.mark.parametrize("N,epi", [(768, 4), (512, 0), (384, 4)])
+def test_gemm_fused_bias_grad(N, epi):
+    """dbias[n] += sum_m C[m][n] of the stored bf16 output: fused into the ping-pong epilogue (N % 256 == 0)
+    and by a column-sum pass otherwise; same result either way."""
+    M, K = 576, 256  # a partial 256-row tile
+    g = torch.Generator().manual_seed(N + epi)
+    A = bf(torch.randn(M, K, generator=g)).to(dev)
+    Bm = bf(torch.randn(K, N, generator=g) * 0.1).to(dev)
+    aux = bf(torch.rand(M, N, generator=g)).to(dev)
+    C = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    db0 = torch.randn(N, generator=g)
+    db = db0.to(dev)
+    L().gemm(1, epi, M, N, K, A, K, Bm, N, C, N, aux=aux if epi == 4 else None, ldaux=N, dbias=db)
+    torch.cuda.synchronize()
+    ref = db0.double() + C.cpu().double().sum(0)
+    assert rel_err(db.cpu(), ref) < 1e-5
