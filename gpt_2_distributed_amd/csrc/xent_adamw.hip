@@ -114,6 +114,82 @@ __global__ __launch_bounds__(256) void xent_fwd_kernel(const TL* __restrict__ lo
   }
 }
 
+// Register-resident variant (the bf16 GPT-2 head: V = 50257): one 1024-thread block per row holds
+// the whole row in registers (NCH chunks of 8 logits per thread), so the logits are read from HBM
+// ONCE: max -> sum of exp -> lse -> dlogits all from registers (the two-pass kernel above re-reads a
+// 100 KB row that no longer sits in L2 when its second pass starts: 3 passes of HBM traffic).
+template <int NCH>
+__global__ __launch_bounds__(1024) void xent_row_kernel(const bf16* __restrict__ logits, int ld,
+                                                        const int64_t* __restrict__ labels,
+                                                        float* __restrict__ loss_rows, float* __restrict__ lse_out,
+                                                        bf16* __restrict__ dlogits, int ldd, int V, int ignore_index) {
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const bf16* lp = logits + (size_t)row * ld;
+  __shared__ float red[16];
+  __shared__ float s_bcast;
+  bf16x8 raw[NCH];  // the row, packed (4 VGPRs per chunk of 8)
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int c = 8 * (tid + 1024 * i);
+    raw[i] = c < ld ? *reinterpret_cast<const bf16x8*>(lp + c) : bf16x8{};
+    if (c + 8 > V) {  // the padding (and the unread tail) never wins the max and has exp(.) = 0
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (c + j >= V) raw[i][j] = (bf16)(-INFINITY);
+    }
+  }
+  auto val = [&](int i, int j) { return bf2f(raw[i][j]); };
+  float m = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < NCH; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m = fmaxf(m, val(i, j));
+  m = wave_max(m);
+  if (lane == 0) red[w] = m;
+  __syncthreads();
+  if (tid == 0) {
+    float t = red[0];
+    for (int k = 1; k < 16; ++k) t = fmaxf(t, red[k]);
+    s_bcast = t;
+  }
+  __syncthreads();
+  const float mx = s_bcast;
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < NCH; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sum += __expf(val(i, j) - mx);  // exp(-inf) = 0 for the padding
+  sum = wave_sum(sum);
+  __syncthreads();  // s_bcast consumed
+  if (lane == 0) red[w] = sum;
+  __syncthreads();
+  if (tid == 0) {
+    float t = 0.f;
+    for (int k = 0; k < 16; ++k) t += red[k];
+    const float lse = mx + __logf(t);
+    s_bcast = lse;
+    lse_out[row] = lse;
+    const int64_t y = labels[row];
+    loss_rows[row] = (y == ignore_index) ? 0.f : lse - bf2f(lp[y]);
+  }
+  __syncthreads();
+  if (!dlogits) return;
+  const float lse = s_bcast;
+  const int64_t y = labels[row];
+  const bool ign = (y == ignore_index);
+  bf16* dp = dlogits + (size_t)row * ldd;
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int c = 8 * (tid + 1024 * i);
+    if (c >= ldd) continue;
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(ign ? 0.f : __expf(val(i, j) - lse));
+    if (!ign && (uint32_t)(y - c) < 8u) o[y - c] = f2bf(bf2f(o[y - c]) - 1.f);
+    *reinterpret_cast<bf16x8*>(dp + c) = o;
+  }
+}
+
 // loss = sum(loss_rows)/count(valid); inv_count = 1/count (the dlogits scale for backward).
 __global__ __launch_bounds__(1024) void xent_finalize_kernel(const float* __restrict__ loss_rows,
                                                             const int64_t* __restrict__ labels, int M, int ignore_index,
@@ -230,6 +306,16 @@ static int xent_fwd_t(const TL* logits, int ld, const int64_t* labels, float* lo
   GPT2MI_REQUIRE(ld % 8 == 0 && ld >= V && (dlogits == nullptr || (ldd % 8 == 0 && ldd >= V)),
                  "xent_fwd: row strides must be multiples of 8 and >= V (ld=%d ldd=%d V=%d)", ld, ldd, V);
   hipStream_t s = (hipStream_t)stream;
+  const int nch = (max(ld, dlogits ? ldd : 0) + 8 * 1024 - 1) / (8 * 1024);
+  if constexpr (sizeof(TL) == 2) {
+    if (nch == 7) {  // GPT-2 vocab under autocast: one register-resident pass over the bf16 logits
+      xent_row_kernel<7><<<M, 1024, 0, s>>>(logits, ld, labels, loss_rows, lse, dlogits, ldd, V, ignore_index);
+      int rc = gpt2mi::check_launch("xent_row");
+      if (rc) return rc;
+      xent_finalize_kernel<<<1, 1024, 0, s>>>(loss_rows, labels, M, ignore_index, loss, inv_count);
+      return gpt2mi::check_launch("xent_finalize");
+    }
+  }
   xent_fwd_kernel<TL><<<M, 256, 0, s>>>(logits, ld, labels, loss_rows, lse, dlogits, ldd, V, ignore_index);
   int rc = gpt2mi::check_launch("xent_fwd");
   if (rc) return rc;
