@@ -36,6 +36,7 @@ _SIGS = {
     "gpt2mi_grad_norm": [_p, _c_size, _c_float, _p, _p, _p],
     "gpt2mi_norm_partials_size": [],
     "gpt2mi_cast_f32_bf16": [_p, _p, _c_size, _p],
+    "gpt2mi_transpose_bf16": [_p, _p, _c_int, _c_int, _c_int, _c_int, _p],
     "gpt2mi_scale_mul": [_p, _p, _p, _p],
     "gpt2mi_memset_zero": [_p, _c_size, _p],
     "gpt2mi_set_gemm_impl": [_c_int],
@@ -205,6 +206,10 @@ def norm_partials_size() -> int:
 
 def cast_f32_bf16(x, y, n):
     _call("gpt2mi_cast_f32_bf16", _ptr(x), _ptr(y), n, _stream())
+
+
+def transpose_bf16(src, dst, R, C, ld_src=None, ld_dst=None):
+    _call("gpt2mi_transpose_bf16", _ptr(src), _ptr(dst), R, C, ld_src or C, ld_dst or R, _stream())
 
 
 def scale_mul(a, b, out):

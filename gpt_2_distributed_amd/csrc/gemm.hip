@@ -266,6 +266,7 @@ GPT2MI_EXPORT int gpt2mi_gemm(int layout, int epilogue, int M, int N, int K, con
     case 0 * 16 + EPI_F32: return launch<false, false, EPI_F32>(P, splits, s);
     case 0 * 16 + EPI_RESID: return launch<false, false, EPI_RESID>(P, splits, s);
     case 0 * 16 + EPI_GELU: return launch<false, false, EPI_GELU>(P, splits, s);
+    case 0 * 16 + EPI_GELU_BWD: return launch<false, false, EPI_GELU_BWD>(P, splits, s);
     case 1 * 16 + EPI_BF16: return launch<false, true, EPI_BF16>(P, splits, s);
     case 1 * 16 + EPI_F32: return launch<false, true, EPI_F32>(P, splits, s);
     case 1 * 16 + EPI_GELU_BWD: return launch<false, true, EPI_GELU_BWD>(P, splits, s);

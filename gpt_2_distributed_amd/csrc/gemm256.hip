@@ -187,6 +187,7 @@ int gemm256_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t 
     case 0 * 16 + EPI_F32: return launch<false, false, EPI_F32>(P, s, 1);
     case 0 * 16 + EPI_RESID: return launch<false, false, EPI_RESID>(P, s, 1);
     case 0 * 16 + EPI_GELU: return launch<false, false, EPI_GELU>(P, s, 1);
+    case 0 * 16 + EPI_GELU_BWD: return launch<false, false, EPI_GELU_BWD>(P, s, 1);
     case 1 * 16 + EPI_BF16: return launch<false, true, EPI_BF16>(P, s, 1);
     case 1 * 16 + EPI_F32: return launch<false, true, EPI_F32>(P, s, 1);
     case 1 * 16 + EPI_GELU_BWD: return launch<false, true, EPI_GELU_BWD>(P, s, 1);

@@ -159,6 +159,12 @@ class Engine:
         arena = model.arena
         self.grad = torch.zeros_like(arena)
         self.shadow = torch.empty(arena.numel(), dtype=BF16, device=self.device)
+        # W^T of every 2-D weight (same slot offsets, [in][out] row-major): the backward dgrad
+        # dX = dY.W then runs as the forward-layout GEMM with both operands k-contiguous
+        self.shadowT = torch.empty(arena.numel(), dtype=BF16, device=self.device)
+        self._t_weights = [n for n, sl in self.layout.slots.items()
+                           if len(sl.shape) == 2 and n != "lm_head.weight" and "wpe" not in n]
+        self._shadowT_stale = True
         self._shadow_versions = None
         self._ws: Dict[tuple, Workspace] = {}
         self._fwd_token = 0
@@ -200,12 +206,35 @@ class Engine:
         own pass; after any other in-place update (torch optimizers, load_state_dict) it is re-cast."""
         K.cast_f32_bf16(self.model.arena, self.shadow, self.model.arena.numel())
         self._shadow_versions = self._versions()
+        self._shadowT_stale = True
 
     def _versions(self):
         return tuple(p._version for p in self._params)
 
     def mark_shadow_fresh(self):
         self._shadow_versions = self._versions()
+        self._shadowT_stale = True
+
+    def _rows(self, name):
+        sl = self.layout.slots[name]
+        return sl.reserved // sl.shape[1]  # wte: the vocab-padded row count
+
+    def wT_ok(self, name) -> bool:
+        sl = self.layout.slots[name]
+        return self._rows(name) % 64 == 0 and sl.shape[1] % 64 == 0
+
+    def _refresh_shadowT(self):
+        for n in self._t_weights:
+            if self.wT_ok(n):
+                sl = self.layout.slots[n]
+                R, Cc = self._rows(n), sl.shape[1]
+                K.transpose_bf16(self.shadow[sl.offset:sl.offset + R * Cc], self.shadowT[sl.offset:sl.offset + R * Cc],
+                                 R, Cc)
+        self._shadowT_stale = False
+
+    def wT16(self, name):  # bf16 W^T view (flat, [in][out_padded])
+        s = self.layout.slots[name]
+        return self.shadowT[s.offset:s.offset + s.reserved]
 
     def _maybe_refresh_shadow(self):
         if self._versions() != self._shadow_versions:
@@ -308,6 +337,8 @@ class Engine:
         act = self.compute_dtype()
         if act == BF16:
             self._maybe_refresh_shadow()
+            if self._shadowT_stale and need_grad:
+                self._refresh_shadowT()
         ws = self.workspace(B, T, act)
         W = lambda n: self.w(n, act)  # noqa: E731
         pr, pa = self._dropout()
@@ -380,10 +411,16 @@ class Engine:
                 K.gemm(K.WGRAD, K.EPI_ATOMIC, m, n, M, a, lda, b, ldb, out, n, splits=S)
         x = ws.x
 
+        def dgrad(out, dy, wname, n_in, n_out, epi=K.EPI_BF16, **kw):
+            # dX[M][n_in] = dY[M][n_out] . W[n_out][n_in]: the forward layout against W^T when it exists
+            if act == BF16 and self.wT_ok(wname):
+                K.gemm(K.FWD, epi, M, n_in, n_out, dy, n_out, self.wT16(wname), n_out, out, n_in, **kw)
+            else:
+                K.gemm(K.DGRAD, epi, M, n_in, n_out, dy, n_out, W(wname), n_in, out, n_in, **kw)
+
         # lm_head (tied): dlnf = dlogits @ wte ; dwte (+)= dlogits^T @ lnf
         with self._probe("lm_head_dgrad"):
-            K.gemm(K.DGRAD, K.EPI_BF16, M, C, Vp, ws.dlogits, Vp, W("transformer.wte.weight"), C, ws.dln, C,
-                   alpha_dev=ws.dscale)
+            dgrad(ws.dln, ws.dlogits, "transformer.wte.weight", C, Vp, K.EPI_BF16, alpha_dev=ws.dscale)
         wte_g = self.layout.padded_view(self.grad, "transformer.wte.weight", Vp)
         with self._probe("lm_head_wgrad"):
             if C % 256 == 0 and act == BF16:
@@ -402,19 +439,19 @@ class Engine:
             A = ws.blocks[l]
             pre = f"transformer.h.{l}."
             # ---- MLP: dY2 = dres_bf (fc2 dropout applied), db2 done by the LN bwd above
-            K.gemm(K.DGRAD, K.EPI_GELU_BWD, M, 4 * C, C, ws.dres_bf, C, W(pre + "mlp.fc2.weight"), 4 * C,
-                   ws.dU, 4 * C, aux=A.dgelu, ldaux=4 * C, dbias=self.g(pre + "mlp.fc1.bias"))
+            dgrad(ws.dU, ws.dres_bf, pre + "mlp.fc2.weight", 4 * C, C, K.EPI_GELU_BWD, aux=A.dgelu, ldaux=4 * C,
+                  dbias=self.g(pre + "mlp.fc1.bias"))
             wgrad(C, 4 * C, ws.dres_bf, C, A.h, 4 * C, self.g(pre + "mlp.fc2.weight"))
-            K.gemm(K.DGRAD, K.EPI_BF16, M, C, 4 * C, ws.dU, 4 * C, W(pre + "mlp.fc1.weight"), C, ws.dln, C)
+            dgrad(ws.dln, ws.dU, pre + "mlp.fc1.weight", C, 4 * C)
             wgrad(4 * C, C, ws.dU, 4 * C, A.ln2, C, self.g(pre + "mlp.fc1.weight"))
             K.layernorm_bwd(A.xmid, self.p(pre + "ln2.weight"), A.m2, A.r2, ws.dln, ws.dres, self.g(pre + "ln2.weight"),
                             self.g(pre + "ln2.bias"), ws.dres_bf, self.g(pre + "attn.proj.bias"), M, C, pr,
                             seeds[("proj", l)])
             # ---- attention
-            K.gemm(K.DGRAD, K.EPI_BF16, M, C, C, ws.dres_bf, C, W(pre + "attn.proj.weight"), C, ws.dln, C)
+            dgrad(ws.dln, ws.dres_bf, pre + "attn.proj.weight", C, C)
             wgrad(C, C, ws.dres_bf, C, A.ao, C, self.g(pre + "attn.proj.weight"))
             K.attn_bwd(A.qkv, A.ao, ws.dln, A.lse, ws.delta, ws.dqkv, B, T, H, C // H, pa, seeds[("attn", l)])
-            K.gemm(K.DGRAD, K.EPI_BF16, M, C, 3 * C, ws.dqkv, 3 * C, W(pre + "attn.qkv.weight"), C, ws.dln, C)
+            dgrad(ws.dln, ws.dqkv, pre + "attn.qkv.weight", C, 3 * C)
             wgrad(3 * C, C, ws.dqkv, 3 * C, A.ln1, C, self.g(pre + "attn.qkv.weight"))
             K.colsum_bf16(ws.dqkv, self.g(pre + "attn.qkv.bias"), M, 3 * C, 3 * C)
             if l > 0:

@@ -127,6 +127,9 @@ int gpt2mi_xent_fwd_f32(const float* logits, int ld, const int64_t* labels, floa
  * 1 = always the 128x128 kernel. */
 void gpt2mi_set_gemm_impl(int impl);
 
+/* dst[c][r] = src[r][c] for a bf16 [R][C] matrix (R, C multiples of 64): the transposed weight shadow
+ * the backward dgrad GEMMs read in the forward (k-contiguous) layout. */
+int gpt2mi_transpose_bf16(const uint16_t* src, uint16_t* dst, int R, int C, int ld_src, int ld_dst, void* stream);
 int gpt2mi_cast_f32_bf16(const float* x, uint16_t* y, size_t n, void* stream);
 int gpt2mi_scale_mul(const float* a, const float* b, float* out, void* stream);
 int gpt2mi_memset_zero(void* ptr, size_t bytes, void* stream);

@@ -29,6 +29,7 @@ SHAPES = {
     "fc1_wgrad": (2, K.EPI_F32, 3072, 768, 65536),
     "qkv_wgrad": (2, K.EPI_F32, 2304, 768, 65536),
     "proj_wgrad": (2, K.EPI_F32, 768, 768, 65536),
+    "sq8k_wgrad": (2, K.EPI_F32, 8192, 8192, 8192),
 }
 
 
