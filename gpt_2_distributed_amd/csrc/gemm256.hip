@@ -7,7 +7,7 @@
 // barrier per K-tile. Measured alternatives that were slower on MI355X (tools/kbench.py): a 4-stage
 // BK=32 ring with counted vmcnt (twice the barriers per MFMA) and register double-buffering of
 // the fragments (the compiler already overlaps the ds_reads; +70 VGPRs).
-// Split-K (wgrad): blockIdx.y selects a K range; each split writes its fp32 partial tile to a slab
+// Split-K (wgrad): the block's item index selects a K range; each split writes its fp32 partial tile to a slab
 // and gpt2mi_gemm_wgrad sums the slabs into the gradient in a second, deterministic pass.
 // The DMA destination is lane-linear, so the bank-conflict XOR swizzle is applied on the SOURCE
 // address and undone on the ds_read:
@@ -79,7 +79,12 @@ __global__ __launch_bounds__(kThreads, 1) void gemm256_kernel(GemmParams P) {
 
   const int tiles_m = (P.M + BM - 1) / BM, tiles_n = P.N / BN;
   const int ntiles = tiles_m * tiles_n;
-  const int pid = xcd_remap(blockIdx.x, ntiles);
+  // 1-D grid over (split, tile) items, split-major: the XCD remap gives each XCD a contiguous item range,
+  // so the blocks of one K split (which share its A and B token rows) run out of one L2
+  const int nsplit = (P.K + P.k_per_split - 1) / P.k_per_split;
+  const int item = xcd_remap(blockIdx.x, ntiles * nsplit);
+  const int split = item / ntiles;
+  const int pid = item - split * ntiles;
   constexpr int GM = 4;
   const int group = pid / (GM * tiles_n);
   const int first_m = group * GM;
@@ -87,7 +92,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm256_kernel(GemmParams P) {
   const int tm = first_m + (pid % (GM * tiles_n)) % gsz;
   const int tn = (pid % (GM * tiles_n)) / gsz;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int kbeg = blockIdx.y * P.k_per_split;
+  const int kbeg = split * P.k_per_split;
   const int nk = (min(P.K, kbeg + P.k_per_split) - kbeg) / BK;
 
   f32x4 acc[8][4];
@@ -148,7 +153,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm256_kernel(GemmParams P) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * alpha + bias[j][r];
       if constexpr (EPI == EPI_SLAB) {  // split-K partial: plain 16-B store into slab blockIdx.y
-        float* slab = reinterpret_cast<float*>(P.C) + (size_t)blockIdx.y * P.M * P.ldc;
+        float* slab = reinterpret_cast<float*>(P.C) + (size_t)split * P.M * P.ldc;
         *reinterpret_cast<f32x4*>(slab + (size_t)gm * P.ldc + gn) = v;
       } else {
         epilogue_store<EPI>(P, gm, gn, v);
@@ -159,7 +164,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm256_kernel(GemmParams P) {
 
 template <bool A_T, bool B_T, int EPI>
 int launch(const GemmParams& P, hipStream_t s, int splits) {
-  dim3 grid(((P.M + BM - 1) / BM) * (P.N / BN), splits);
+  dim3 grid(((P.M + BM - 1) / BM) * (P.N / BN) * splits);
   gemm256_kernel<A_T, B_T, EPI><<<grid, kThreads, 0, s>>>(P);
   return gpt2mi::check_launch("gemm256");
 }

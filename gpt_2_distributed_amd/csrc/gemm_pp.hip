@@ -169,7 +169,12 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
 
   const int tiles_m = (P.M + BM - 1) / BM, tiles_n = P.N / BN;
   const int ntiles = tiles_m * tiles_n;
-  const int pid = xcd_remap(blockIdx.x, ntiles);
+  // 1-D grid over (split, tile) items, split-major: the XCD remap gives each XCD a contiguous item range,
+  // so the blocks of one K split (which share its A and B token rows) run out of one L2
+  const int nsplit = (P.K + P.k_per_split - 1) / P.k_per_split;
+  const int item = xcd_remap(blockIdx.x, ntiles * nsplit);
+  const int split = item / ntiles;
+  const int pid = item - split * ntiles;
   constexpr int GM = 4;
   const int group = pid / (GM * tiles_n);
   const int first_m = group * GM;
@@ -177,7 +182,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   const int tm = first_m + (pid % (GM * tiles_n)) % gsz;
   const int tn = (pid % (GM * tiles_n)) / gsz;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int kbeg = blockIdx.y * P.k_per_split;
+  const int kbeg = split * P.k_per_split;
   const int nk = (min(P.K, kbeg + P.k_per_split) - kbeg) / BK;  // even (host-checked)
 
   f32x4 acc[2][2][4][2];
@@ -292,7 +297,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] += bias[e];
       if constexpr (EPI == EPI_SLAB) {
-        float* slab = reinterpret_cast<float*>(P.C) + (size_t)blockIdx.y * P.M * P.ldc;
+        float* slab = reinterpret_cast<float*>(P.C) + (size_t)split * P.M * P.ldc;
         *reinterpret_cast<f32x4*>(slab + (size_t)gm * P.ldc + gn) = v;
       } else {
         const f32x4 o = epilogue_apply<EPI>(P, gm, gn, v, kOpnd ? opnd[it] : f32x4{0.f, 0.f, 0.f, 0.f});
@@ -341,7 +346,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
 // k-contiguous forward operands).
 template <bool A_T, bool B_T, int EPI, int MAP = (A_T ? 1 : 0) | (B_T ? 2 : 0)>
 int launch(const GemmParams& P, hipStream_t s, int splits) {
-  dim3 grid(((P.M + BM - 1) / BM) * (P.N / BN), splits);
+  dim3 grid(((P.M + BM - 1) / BM) * (P.N / BN) * splits);
   gemm_pp_kernel<A_T, B_T, EPI, MAP><<<grid, kThreads, 0, s>>>(P);
   return gpt2mi::check_launch("gemm_pp");
 }
