@@ -30,6 +30,11 @@ SHAPES = {
     "qkv_wgrad": (2, K.EPI_F32, 2304, 768, 65536),
     "proj_wgrad": (2, K.EPI_F32, 768, 768, 65536),
     "sq8k_wgrad": (2, K.EPI_F32, 8192, 8192, 8192),
+    # per-tile fixed cost: the same 2304 x 65536 output at three depths
+    "qkv_k768": (0, K.EPI_BF16, 65536, 2304, 768),
+    "qkv_k1536": (0, K.EPI_BF16, 65536, 2304, 1536),
+    "qkv_k3072": (0, K.EPI_BF16, 65536, 2304, 3072),
+    "qkv_k768_f32": (0, K.EPI_F32, 65536, 2304, 768),
 }
 
 

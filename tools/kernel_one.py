@@ -1,0 +1,52 @@
+"""Launch ONE of bench.py's probed kernels a few times on step-shaped inputs (GPT-2 124M, B=64, T=1024,
+dropout 0.1), for the rocprofv3 --pmc traffic passes (tools/pmc_traffic.sh -> profiles/traffic.json).
+
+    python tools/kernel_one.py <lm_head_fwd|lm_head_dgrad|lm_head_wgrad|fc1_fwd|attn_fwd> [reps]
+"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from gpt_2_distributed_amd import _lib as K  # noqa: E402
+
+dev = "cuda"
+M, C, Vp, V, B, T, H = 65536, 768, 50432, 50257, 64, 1024, 12
+
+
+def r(*s):
+    return (torch.randn(*s, device=dev) * 0.5).to(torch.bfloat16)
+
+
+def make(name):
+    if name == "lm_head_fwd":
+        a, w, out = r(M, C), r(Vp, C), torch.empty(M, Vp, dtype=torch.bfloat16, device=dev)
+        return lambda: K.gemm(K.FWD, K.EPI_BF16, M, Vp, C, a, C, w, C, out, Vp)
+    if name == "lm_head_dgrad":  # forward layout against the transposed wte shadow
+        dl, wt, out = r(M, Vp), r(C, Vp), torch.empty(M, C, dtype=torch.bfloat16, device=dev)
+        return lambda: K.gemm(K.FWD, K.EPI_BF16, M, C, Vp, dl, Vp, wt, Vp, out, C)
+    if name == "lm_head_wgrad":
+        dl, x, g = r(M, Vp), r(M, C), torch.zeros(Vp, C, device=dev)
+        sp = K.wgrad_splits(Vp, C, M)
+        ws = torch.empty(sp * Vp * C, device=dev)
+        return lambda: K.gemm_wgrad(Vp, C, M, dl, Vp, x, C, g, C, workspace=ws, splits=sp)
+    if name == "fc1_fwd":
+        a, w = r(M, C), r(4 * C, C)
+        bias = torch.zeros(4 * C, device=dev)
+        h, dg = (torch.empty(M, 4 * C, dtype=torch.bfloat16, device=dev) for _ in range(2))
+        return lambda: K.gemm(K.FWD, K.EPI_GELU, M, 4 * C, C, a, C, w, C, h, 4 * C, bias=bias, aux=dg, ldaux=4 * C,
+                              p_drop=0.1, seed=3)
+    if name == "attn_fwd":
+        qkv, out = r(M, 3 * C), torch.empty(M, C, dtype=torch.bfloat16, device=dev)
+        lse = torch.empty(B * H, T, device=dev)
+        return lambda: K.attn_fwd(qkv, out, lse, B, T, H, C // H, 0.1, 5)
+    raise SystemExit(f"unknown kernel {name}")
+
+
+if __name__ == "__main__":
+    K.load()
+    fn = make(sys.argv[1])
+    for _ in range(int(sys.argv[2]) if len(sys.argv) > 2 else 3):
+        fn()
+    torch.cuda.synchronize()
