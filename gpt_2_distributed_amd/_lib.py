@@ -13,7 +13,8 @@ from typing import Optional
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libgpt2mi.so")
+# GPT2MI_LIB: an alternative build of the same library (A/B kernel experiments, tools/kbench.py)
+LIB_PATH = os.environ.get("GPT2MI_LIB") or os.path.join(_HERE, "libgpt2mi.so")
 
 _c_int, _c_float, _c_size, _c_u64, _p = ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_void_p
 

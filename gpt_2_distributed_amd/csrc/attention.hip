@@ -119,6 +119,7 @@ __device__ __forceinline__ void attn_block(int& bh, int& blk) {
 // drop_hash(seed, (bh*T + (q & ~16))*T + key) — queries q and q^16 of one key share a hash.
 
 // ---------------------------------------------------------------------------------------------
+template <bool DROP>
 __global__ __launch_bounds__(kThreads, 3) void attn_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
                                                                float* __restrict__ lse, int T, int H, float scale,
                                                                uint64_t seed, uint32_t thr, float inv_keep) {
@@ -143,12 +144,16 @@ __global__ __launch_bounds__(kThreads, 3) void attn_fwd_kernel(const bf16* __res
       qf[qg][kk] = *reinterpret_cast<const bf16x8*>(
           base + (size_t)min(q_lo + 16 * qg + (lane & 15), T - 1) * ld + h * D + 32 * kk + 8 * g);
   const float sl2 = scale * kLog2e;
-  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
-  f32x4 o[2][4];
+  float m[2] = {-INFINITY, -INFINITY};
+  // o[qg][4] holds the row sums l = P.1 of the group's queries: one more PV-shaped MFMA against a
+  // ones operand (the MFMA pipe has slack; 32 VALU adds per tile do not). Every row of it is l.
+  f32x4 o[2][5];
 #pragma unroll
   for (int qg = 0; qg < 2; ++qg)
 #pragma unroll
-    for (int f = 0; f < 4; ++f) o[qg][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int f = 0; f < 5; ++f) o[qg][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bf16 one = (bf16)1.f;
+  const bf16x8 ones = {one, one, one, one, one, one, one, one};
 
   u32x4 rk[2], rv[2];
   const bf16* kbase = base + C + h * D;
@@ -205,25 +210,25 @@ __global__ __launch_bounds__(kThreads, 3) void attn_fwd_kernel(const bf16* __res
         if (!__all(cand <= m[qg] + kRescaleThr)) {
           const float mn = fmaxf(m[qg], cand);  // finite: tile 0 holds key 0, visible to every query
           const float corr = __builtin_amdgcn_exp2f(m[qg] - mn);
-          l[qg] *= corr;
 #pragma unroll
           for (int f = 0; f < 4; ++f)
 #pragma unroll
             for (int r = 0; r < 4; ++r) o[qg][f][r] *= corr;
+          o[qg][4][0] *= corr;  // only row 0 of the row-sum accumulator is read
           m[qg] = mn;
         }
-        float rs = 0.f;  // per-lane partial row sum (the cross-lane sum is taken once, at the end)
 #pragma unroll
         for (int fi = 0; fi < 4; ++fi)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float pv = __builtin_amdgcn_exp2f(fmaf(s[qg][fi][r], sl2, -m[qg]));
-            rs += pv;
-            s[qg][fi][r] = pv;
-          }
-        l[qg] += rs;
+          for (int r = 0; r < 4; ++r) s[qg][fi][r] = __builtin_amdgcn_exp2f(fmaf(s[qg][fi][r], sl2, -m[qg]));
       }
-      if (thr) {  // dropout on P (not on the normaliser; the 1/(1-p) goes into the final scale): one
+      // row sums before dropout (the normaliser is the undropped softmax denominator)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        o[0][4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pack_perm(s[0], kk), o[0][4], 0, 0, 0);
+        o[1][4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pack_perm(s[1], kk), o[1][4], 0, 0, 0);
+      }
+      if constexpr (DROP) {  // dropout on P (not on the normaliser; the 1/(1-p) goes into the final scale): one
                   // hash per (q, q^16) pair of a key
         const uint32_t s32 = seed32(seed);
         const uint32_t pbase = ((uint32_t)bh * T + q_lo + (lane & 15)) * (uint32_t)T + k_lo + 4 * g;
@@ -258,14 +263,14 @@ __global__ __launch_bounds__(kThreads, 3) void attn_fwd_kernel(const bf16* __res
 #pragma unroll
   for (int qg = 0; qg < 2; ++qg) {
     const int q = q_lo + 16 * qg + (lane & 15);
-    l[qg] = xor_sum(l[qg]);
-    const float il = (thr ? inv_keep : 1.f) / l[qg];
+    const float lq = o[qg][4][0];
+    const float il = (DROP ? inv_keep : 1.f) / lq;
     bf16* op = out + ((size_t)b * T + q) * C + h * D;
 #pragma unroll
     for (int fd = 0; fd < 4; ++fd)
       *reinterpret_cast<bf16x4*>(op + 16 * fd + 4 * g) = bf16x4{f2bf(o[qg][fd][0] * il), f2bf(o[qg][fd][1] * il),
                                                                 f2bf(o[qg][fd][2] * il), f2bf(o[qg][fd][3] * il)};
-    if (g == 0) lse[(size_t)bh * T + q] = (m[qg] + log2f(l[qg])) / kLog2e;  // natural-log LSE of scaled scores
+    if (g == 0) lse[(size_t)bh * T + q] = (m[qg] + log2f(lq)) / kLog2e;  // natural-log LSE of scaled scores
   }
 }
 
@@ -603,9 +608,14 @@ GPT2MI_EXPORT int gpt2mi_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse
   GPT2MI_REQUIRE(T % 64 == 0 && T > 0, "attn_fwd: T=%d must be a multiple of 64", T);
   const float scale = 1.f / sqrtf((float)head_dim);
   dim3 grid((T + BQ - 1) / BQ, B * H);
-  attn_fwd_kernel<<<grid, kThreads, 0, (hipStream_t)stream>>>((const bf16*)qkv, (bf16*)out, lse, T, H, scale, seed,
-                                                              drop_threshold(p_drop),
-                                                              p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f);
+  const uint32_t thr = drop_threshold(p_drop);
+  const float ik = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+  if (thr)
+    attn_fwd_kernel<true><<<grid, kThreads, 0, (hipStream_t)stream>>>((const bf16*)qkv, (bf16*)out, lse, T, H, scale,
+                                                                      seed, thr, ik);
+  else
+    attn_fwd_kernel<false><<<grid, kThreads, 0, (hipStream_t)stream>>>((const bf16*)qkv, (bf16*)out, lse, T, H, scale,
+                                                                       seed, thr, ik);
   return gpt2mi::check_launch("attn_fwd");
 }
 

@@ -252,7 +252,9 @@ def test_attention_fwd_bwd(B, T, H):
     assert rel_err(out.cpu().float(), yref) < 6e-3
     s = (q @ k.transpose(-2, -1)) / 8.0
     s = s.masked_fill(~torch.tril(torch.ones(T, T, dtype=torch.bool)), float("-inf"))
-    assert rel_err(lse.cpu().view(B, H, T), torch.logsumexp(s.detach(), -1)) < 1e-5
+    # the kernel's normaliser is the sum of the bf16-rounded probabilities its PV product uses (row
+    # sums by MFMA): |d lse| ~ 2^-9 / sqrt(3 * keys) relative, not fp32-exact
+    assert rel_err(lse.cpu().view(B, H, T), torch.logsumexp(s.detach(), -1)) < 3e-4
     dout = dy.transpose(1, 2).reshape(B * T, C).contiguous().to(dev)
     dqkv = torch.empty(B * T, 3 * C, dtype=torch.bfloat16, device=dev)
     delta = torch.empty(B * H, T, device=dev)

@@ -40,7 +40,8 @@ def make(name):
     if name == "attn_fwd":
         qkv, out = r(M, 3 * C), torch.empty(M, C, dtype=torch.bfloat16, device=dev)
         lse = torch.empty(B * H, T, device=dev)
-        return lambda: K.attn_fwd(qkv, out, lse, B, T, H, C // H, 0.1, 5)
+        p = float(os.environ.get("ATTN_P", "0.1"))
+        return lambda: K.attn_fwd(qkv, out, lse, B, T, H, C // H, p, 5)
     raise SystemExit(f"unknown kernel {name}")
 
 
