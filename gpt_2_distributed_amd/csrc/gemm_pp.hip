@@ -23,7 +23,7 @@
 //    each half-tile is issued 5-6 phases before its first read: the counted `vmcnt(8)` of every
 //    phase keeps 4 half-tiles (64 KiB per CU) in flight across the barrier and retires exactly the
 //    half-tile the next phase reads (RAW: wait in phase p, read in phase p+1).
-//    DMA for tiles past the end re-load the last tile (never read) so the count stays static.
+//    The last K-tile pair issues no DMA past the end and counts its waits down instead.
 //  * Operand images: k-contiguous operands [128][64] bf16 (128-B rows, 16-B chunk c at c^(row&7),
 //    ds_read_b128); m-contiguous operands [64][128] (256-B rows, chunk c at c^swz(k),
 //    ds_read_b64_tr_b16). The swizzle is applied on the DMA source address (the LDS side of an
@@ -33,6 +33,8 @@
 //    128 rows, 16-B chunk c of row r at c ^ (r & 15): conflict-free both ways), then every wave
 //    reads back whole rows and applies the fused epilogue with full-row coalesced stores (one
 //    store instruction = one 256-column output row).
+#include <type_traits>
+
 #include "common.h"
 #include "gemm_common.h"
 
@@ -139,8 +141,8 @@ __device__ __forceinline__ void mfma_quadrant(f32x4 (&acc)[4][2], const Frags& f
 
 // end of a phase's memory segment: retire the half-tile the next phase reads, then the ping-pong
 // MFMA segment between two barriers
-#define PP_SYNC_MFMA(ACC, NI)                              \
-  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");         \
+#define PP_SYNC_MFMA(ACC, NI, VM)                          \
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM) : "memory"); \
   __builtin_amdgcn_sched_barrier(0);                       \
   __builtin_amdgcn_s_barrier();                            \
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");       \
@@ -195,7 +197,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto kofs = [&](int t) { return kbeg + min(t, nk - 1) * BK; };
+  auto kofs = [&](int t) { return kbeg + t * BK; };
   auto dma_a = [&](int t, int h, char* buf) {
     dma_half<A_T, true, AIL>(P.A, P.lda, m0, h, kofs(t), P.M - 1, buf + (h ? SA1 : SA0), wid, lane);
   };
@@ -218,32 +220,44 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   __builtin_amdgcn_sched_barrier(0);
 
   Frags fr;
-  for (int t = 0; t < nk; t += 2) {
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      char* cur = s ? buf1 : buf0;
-      char* nxt = s ? buf0 : buf1;
-      const int tt = t + s;
-      // phase 1: quadrant (0,0)
-      read_a<A_T>(fr, cur + SA0, wr, lane);
-      read_b<B_T, 0>(fr, cur + SB0, wc, lane);
-      dma_b(tt + 1, 1, nxt);
-      PP_SYNC_MFMA(acc[0][0], 0)
-      // phase 2: quadrant (0,1)
-      read_b<B_T, 1>(fr, cur + SB1, wc, lane);
-      dma_a(tt + 1, 1, nxt);
-      PP_SYNC_MFMA(acc[0][1], 1)
-      // phase 3: quadrant (1,1)
-      read_a<A_T>(fr, cur + SA1, wr, lane);
-      dma_a(tt + 2, 0, cur);
-      PP_SYNC_MFMA(acc[1][1], 1)
-      // phase 4: quadrant (1,0) from registers
-      dma_b(tt + 2, 0, cur);
-      PP_SYNC_MFMA(acc[1][0], 0)
-    }
+  // One K-tile (4 phases) of the pair starting at t: S = 0 / 1 is the tile's parity. In the last pair
+  // (LAST) the DMAs for tiles >= nk are not issued, and each wait retires what the next phase reads
+  // from the real DMAs still outstanding (vmcnt 8,8,6,4 | 2,0,0,0 instead of 8 everywhere): no re-load
+  // traffic, and nothing left in flight for the epilogue to wait for.
+  auto ktile = [&](int t, auto s_c, auto last_c) {
+    constexpr int S = decltype(s_c)::value;
+    constexpr bool LAST = decltype(last_c)::value;
+    constexpr bool next_dma = !LAST || S == 0;  // tile tt + 1 exists
+    constexpr bool next2_dma = !LAST;           // tile tt + 2 exists
+    char* cur = S ? buf1 : buf0;
+    char* nxt = S ? buf0 : buf1;
+    const int tt = t + S;
+    // phase 1: quadrant (0,0)
+    read_a<A_T>(fr, cur + SA0, wr, lane);
+    read_b<B_T, 0>(fr, cur + SB0, wc, lane);
+    if constexpr (next_dma) dma_b(tt + 1, 1, nxt);
+    PP_SYNC_MFMA(acc[0][0], 0, (!LAST || S == 0) ? 8 : 2)
+    // phase 2: quadrant (0,1)
+    read_b<B_T, 1>(fr, cur + SB1, wc, lane);
+    if constexpr (next_dma) dma_a(tt + 1, 1, nxt);
+    PP_SYNC_MFMA(acc[0][1], 1, (!LAST || S == 0) ? 8 : 0)
+    // phase 3: quadrant (1,1)
+    read_a<A_T>(fr, cur + SA1, wr, lane);
+    if constexpr (next2_dma) dma_a(tt + 2, 0, cur);
+    PP_SYNC_MFMA(acc[1][1], 1, !LAST ? 8 : (S == 0 ? 6 : 0))
+    // phase 4: quadrant (1,0) from registers
+    if constexpr (next2_dma) dma_b(tt + 2, 0, cur);
+    PP_SYNC_MFMA(acc[1][0], 0, !LAST ? 8 : (S == 0 ? 4 : 0))
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  for (int t = 0; t < nk - 2; t += 2) {
+    ktile(t, I0{}, std::false_type{});
+    ktile(t, I1{}, std::false_type{});
   }
+  ktile(nk - 2, I0{}, std::true_type{});
+  ktile(nk - 2, I1{}, std::true_type{});
   if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the groups (same barrier count)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail DMAs into LDS have landed
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
 

@@ -24,6 +24,11 @@ SHAPES = {
     "qkv_fwd": (0, K.EPI_BF16, 65536, 2304, 768),
     "fc2_dgelu": (1, K.EPI_GELU_BWD, 65536, 3072, 768),
     "fc1_dgrad": (1, K.EPI_BF16, 65536, 768, 3072),
+    # dgrads as the step runs them (forward layout against the transposed weight shadow)
+    "fc2_dgelu0": (0, K.EPI_GELU_BWD, 65536, 3072, 768),
+    "proj_dgrad0": (0, K.EPI_BF16, 65536, 768, 768),
+    "qkv_dgrad0": (0, K.EPI_BF16, 65536, 768, 2304),
+    "proj_resid": (0, K.EPI_RESID, 65536, 768, 768),
     # weight gradients (layout 2 through gemm_wgrad: split-K slabs + deterministic reduce)
     "lm_wgrad": (2, K.EPI_F32, 50432, 768, 65536),
     "fc1_wgrad": (2, K.EPI_F32, 3072, 768, 65536),
