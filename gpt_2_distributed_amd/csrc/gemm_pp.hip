@@ -368,19 +368,13 @@ int launch(const GemmParams& P, hipStream_t s, int splits) {
 }  // namespace
 
 namespace gpt2mi {
-// N % 256 == 0, every split's K range an even number (>= 2) of 64-deep tiles; layout 2 needs M % 256 == 0.
+// Layouts 0 / 1; N % 256 == 0, every split's K range an even number (>= 2) of 64-deep tiles.
 // Returns -1 when this kernel does not apply (the caller falls back).
 int gemm_pp_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t s, int splits, int map) {
   if (P.N % BN != 0 || P.k_per_split % (2 * BK) != 0 || P.K % (2 * BK) != 0) return -1;
-  if (layout == 2 && P.M % BM != 0) return -1;
-  // wgrad (both operands m-contiguous) stays on the 2-stage gemm256 kernel by default: measured
+  // wgrad (both operands m-contiguous) runs on the 2-stage gemm256 kernel: this one measured
   // 698-721 TF vs 765 TF on the lm_head wgrad, 756 vs 852 on qkv (tools/gemm_probe.py, every map)
-  if (map == 0 && layout == 2) return -1;
-  if (map > 0 && layout == 2 && epilogue == EPI_F32) {  // (map - 1) = A/B interleave bits
-    if (map == 1) return launch<true, true, EPI_F32, 0>(P, s, 1);
-    if (map == 2) return launch<true, true, EPI_F32, 1>(P, s, 1);
-    if (map == 3) return launch<true, true, EPI_F32, 2>(P, s, 1);
-  }
+  if (layout == 2) return -1;
   if (map > 0 && epilogue == EPI_BF16 && layout <= 1) {  // half-tile map experiments (tools/gemm_probe.py)
     if (layout == 0) {
       if (map == 1) return launch<false, false, EPI_BF16, 1>(P, s, 1);
@@ -401,8 +395,6 @@ int gemm_pp_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t 
     case 1 * 16 + EPI_BF16: return launch<false, true, EPI_BF16>(P, s, 1);
     case 1 * 16 + EPI_F32: return launch<false, true, EPI_F32>(P, s, 1);
     case 1 * 16 + EPI_GELU_BWD: return launch<false, true, EPI_GELU_BWD>(P, s, 1);
-    case 2 * 16 + EPI_F32: return launch<true, true, EPI_F32>(P, s, 1);
-    case 2 * 16 + EPI_SLAB: return launch<true, true, EPI_SLAB>(P, s, splits);
     default: return -1;
   }
 }
