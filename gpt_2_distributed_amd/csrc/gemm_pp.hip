@@ -161,8 +161,26 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// Timing instrumentation (tools/gemm_timing.py builds a separate library with -DGEMM_PP_TIMING): wave 0
+// of every block stamps s_memtime at kernel start (0), first operands landed (1), end of the main loop
+// (2) and end of the epilogue (3), plus its HW_ID / XCC_ID, into P.aux (BF16 epilogue only).
+#ifdef GEMM_PP_TIMING
+#define PP_STAMP(I)                                                                                  \
+  if (EPI == EPI_BF16 && P.aux && threadIdx.x == 0) {                                               \
+    uint64_t* ts = reinterpret_cast<uint64_t*>(P.aux) + (size_t)blockIdx.x * 6;                    \
+    ts[I] = __builtin_amdgcn_s_memtime();                                                            \
+    if (I == 0) {                                                                                    \
+      ts[4] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);                                  \
+      ts[5] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20);                                 \
+    }                                                                                                \
+  }
+#else
+#define PP_STAMP(I)
+#endif
+
 template <bool A_T, bool B_T, int EPI, int MAP>
 __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
+  PP_STAMP(0)
   constexpr bool AIL = MAP & 1, BIL = MAP & 2;  // interleaved half-tile maps (A/B experiments)
   __shared__ __attribute__((aligned(1024))) char smem[kLds];
   const int lane = threadIdx.x & 63;
@@ -216,6 +234,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   dma_b(1, 0, buf1);
   asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A_0(0), B_0(0) landed
   __builtin_amdgcn_s_barrier();
+  PP_STAMP(1)
   if (wr == 1) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind group 0
   __builtin_amdgcn_sched_barrier(0);
 
@@ -260,6 +279,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the groups (same barrier count)
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
+  PP_STAMP(2)
 
   // ---- epilogue: acc[mi][ni][i][j][r] = C[m0 + mi*128 + wr*64 + 16i + (l&15)][n0 + ni*128 + wc*32 + 16j + 4(l>>4) + r]
   float alpha = P.alpha;
@@ -353,6 +373,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
       }
     }
   }
+  PP_STAMP(3)
 }
 
 // Default half-tile maps: interleaved for m-contiguous (transposed) operands, contiguous otherwise

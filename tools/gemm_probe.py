@@ -40,6 +40,10 @@ SHAPES = {
     "qkv_k1536": (0, K.EPI_BF16, 65536, 2304, 1536),
     "qkv_k3072": (0, K.EPI_BF16, 65536, 2304, 3072),
     "qkv_k768_f32": (0, K.EPI_F32, 65536, 2304, 768),
+    # per-tile fixed cost on the lm_head width: the same 65536 x 50432 output at three depths
+    "lm_k128": (0, K.EPI_BF16, 65536, 50432, 128),
+    "lm_k256": (0, K.EPI_BF16, 65536, 50432, 256),
+    "lm_k512": (0, K.EPI_BF16, 65536, 50432, 512),
 }
 
 
