@@ -275,31 +275,15 @@ __global__ __launch_bounds__(kThreads, 3) void attn_fwd_kernel(const bf16* __res
 }
 
 // ---------------------------------------------------------------------------------------------
-// delta[bh][t] = sum_d dO[b,t,h,d] * O[b,t,h,d]
-__global__ __launch_bounds__(256) void attn_delta_kernel(const bf16* __restrict__ out, const bf16* __restrict__ dout,
-                                                         float* __restrict__ delta, int B, int T, int H) {
-  const int i = blockIdx.x * 256 + threadIdx.x;  // over B*T*H, (b,t) major
-  if (i >= B * T * H) return;
-  const int h = i % H, bt = i / H, b = bt / T, t = bt % T;
-  const size_t off = (size_t)bt * H * D + h * D;
-  float s = 0.f;
-#pragma unroll
-  for (int c = 0; c < D; c += 8) {
-    bf16x8 a = *reinterpret_cast<const bf16x8*>(out + off + c);
-    bf16x8 d = *reinterpret_cast<const bf16x8*>(dout + off + c);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) s += bf2f(a[j]) * bf2f(d[j]);
-  }
-  delta[((size_t)b * H + h) * T + t] = s;
-}
-
-// ---------------------------------------------------------------------------------------------
 // dQ: query-outer; recomputes P from the saved LSE. dS^T = P^T o (dP^T - delta), dQ^T += K^T dS^T.
+// delta = rowsum(dO o O) of the wave's own queries is formed here (no separate pass) and written out for
+// the dK/dV kernel, which runs after this one.
 template <bool DROP>
 __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const bf16* __restrict__ qkv,
+                                                                  const bf16* __restrict__ out,
                                                                   const bf16* __restrict__ dout,
                                                                   const float* __restrict__ lse,
-                                                                  const float* __restrict__ delta,
+                                                                  float* __restrict__ delta,
                                                                   bf16* __restrict__ dqkv, int T, int H, float scale,
                                                                   uint64_t seed, uint32_t thr, float inv_keep) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * BKV * 128];
@@ -319,17 +303,23 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const bf16* __
 #pragma unroll
   for (int qg = 0; qg < 2; ++qg) {
     const int q = min(q_lo + 16 * qg + (lane & 15), T - 1);
+    float dsum = 0.f;  // this lane's 16 of the 64 dims of dO . O
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
+      const size_t row = ((size_t)b * T + q) * C + h * D + 32 * kk + 8 * g;
       qf[qg][kk] = *reinterpret_cast<const bf16x8*>(base + (size_t)q * ld + h * D + 32 * kk + 8 * g);
-      df[qg][kk] = *reinterpret_cast<const bf16x8*>(dout + ((size_t)b * T + q) * C + h * D + 32 * kk + 8 * g);
+      df[qg][kk] = *reinterpret_cast<const bf16x8*>(dout + row);
+      const bf16x8 of = *reinterpret_cast<const bf16x8*>(out + row);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dsum = fmaf(bf2f(df[qg][kk][e]), bf2f(of[e]), dsum);
       if (DROP) {  // dP' = (dO/(1-p)).V: the keep-scale of dropout folded into dO once per wave
 #pragma unroll
         for (int e = 0; e < 8; ++e) df[qg][kk][e] = f2bf(bf2f(df[qg][kk][e]) * inv_keep);
       }
     }
     lse2[qg] = lse[(size_t)bh * T + q] * kLog2e;
-    dl[qg] = delta[(size_t)bh * T + q];
+    dl[qg] = xor_sum(dsum);  // delta = dO . O (the dropped, normalised output), over the 4 lane groups
+    if (wave_valid && g == 0) delta[(size_t)bh * T + q] = dl[qg];
   }
   const float sl2 = scale * kLog2e;
   f32x4 dq[2][4];
@@ -628,8 +618,15 @@ GPT2MI_EXPORT int gpt2mi_attn_bwd(const uint16_t* qkv, const uint16_t* out, cons
   const float scale = 1.f / sqrtf((float)head_dim);
   const uint32_t thr = drop_threshold(p_drop);
   const float ik = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
-  attn_delta_kernel<<<(B * T * H + 255) / 256, 256, 0, s>>>((const bf16*)out, (const bf16*)dout, delta, B, T, H);
-  int rc = gpt2mi::check_launch("attn_delta");
+  // dQ first: it forms delta (dO . O per query) for the dK/dV kernel
+  const dim3 gq((T + BQ - 1) / BQ, B * H);
+  if (thr)
+    attn_bwd_dq_kernel<true><<<gq, kThreads, 0, s>>>((const bf16*)qkv, (const bf16*)out, (const bf16*)dout, lse, delta,
+                                                     (bf16*)dqkv, T, H, scale, seed, thr, ik);
+  else
+    attn_bwd_dq_kernel<false><<<gq, kThreads, 0, s>>>((const bf16*)qkv, (const bf16*)out, (const bf16*)dout, lse,
+                                                      delta, (bf16*)dqkv, T, H, scale, seed, thr, ik);
+  int rc = gpt2mi::check_launch("attn_bwd_dq");
   if (rc) return rc;
   const dim3 gkv((T + BKB - 1) / BKB, B * H);
   if (thr)
@@ -638,14 +635,5 @@ GPT2MI_EXPORT int gpt2mi_attn_bwd(const uint16_t* qkv, const uint16_t* out, cons
   else
     attn_bwd_dkdv_kernel<false><<<gkv, kThreads, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta,
                                                          (bf16*)dqkv, T, H, scale, seed, thr, ik);
-  rc = gpt2mi::check_launch("attn_bwd_dkdv");
-  if (rc) return rc;
-  const dim3 gq((T + BQ - 1) / BQ, B * H);
-  if (thr)
-    attn_bwd_dq_kernel<true><<<gq, kThreads, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta, (bf16*)dqkv, T,
-                                                     H, scale, seed, thr, ik);
-  else
-    attn_bwd_dq_kernel<false><<<gq, kThreads, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta, (bf16*)dqkv, T,
-                                                      H, scale, seed, thr, ik);
-  return gpt2mi::check_launch("attn_bwd_dq");
+  return gpt2mi::check_launch("attn_bwd_dkdv");
 }
