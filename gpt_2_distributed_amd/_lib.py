@@ -30,7 +30,7 @@ _SIGS = {
     "gpt2mi_gemm": [_c_int, _c_int, _c_int, _c_int, _c_int, _p, _c_int, _p, _c_int, _p, _c_int, _p, _p, _p, _c_int,
                     _c_float, _p, _c_int, _c_int, _c_float, _c_u64, _p, _p],
     "gpt2mi_attn_fwd": [_p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_float, _c_u64, _p],
-    "gpt2mi_attn_bwd": [_p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_float, _c_u64, _p],
+    "gpt2mi_attn_bwd": [_p, _p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_float, _c_u64, _p],
     "gpt2mi_xent_fwd": [_p, _c_int, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _p, _p, _p],
     "gpt2mi_adamw": [_p, _p, _p, _p, _p, _c_size, _c_float, _c_float, _c_float, _c_float, _c_float, _c_int,
                      _c_float, _p, _p, _p],
@@ -44,7 +44,7 @@ _SIGS = {
     "gpt2mi_gemm_f32": [_c_int, _c_int, _c_int, _c_int, _c_int, _p, _c_int, _p, _c_int, _p, _c_int, _p, _p, _p,
                         _c_int, _c_float, _p, _c_int, _c_int, _c_float, _c_u64, _p, _p],
     "gpt2mi_attn_fwd_f32": [_p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_float, _c_u64, _p],
-    "gpt2mi_attn_bwd_f32": [_p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_float, _c_u64, _p],
+    "gpt2mi_attn_bwd_f32": [_p, _p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_float, _c_u64, _p],
     "gpt2mi_layernorm_bwd_f32": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_float, _c_u64, _c_int,
                                  _p],
     "gpt2mi_colsum_f32": [_p, _p, _c_int, _c_int, _c_int, _p],
@@ -182,9 +182,10 @@ def attn_fwd(qkv, out, lse, B, T, H, D, p_drop=0.0, seed=0):
     _call("gpt2mi_attn_fwd_f32" if _f32(qkv) else "gpt2mi_attn_fwd", _ptr(qkv), _ptr(out), _ptr(lse), B, T, H, D, p_drop, seed, _stream())
 
 
-def attn_bwd(qkv, out, dout, lse, delta, dqkv, B, T, H, D, p_drop=0.0, seed=0):
-    _call("gpt2mi_attn_bwd_f32" if _f32(qkv) else "gpt2mi_attn_bwd", _ptr(qkv), _ptr(out), _ptr(dout), _ptr(lse), _ptr(delta), _ptr(dqkv), B, T, H, D,
-          p_drop, seed, _stream())
+def attn_bwd(qkv, out, dout, lse, delta, dqkv, B, T, H, D, p_drop=0.0, seed=0, colsum=None):
+    """colsum: optional fp32 [B*T/32, 3C] partial column sums of dqkv (bf16 path; sum rows with colsum_bf16)."""
+    _call("gpt2mi_attn_bwd_f32" if _f32(qkv) else "gpt2mi_attn_bwd", _ptr(qkv), _ptr(out), _ptr(dout), _ptr(lse),
+          _ptr(delta), _ptr(dqkv), _ptr(colsum), B, T, H, D, p_drop, seed, _stream())
 
 
 def xent_fwd(logits, ld, labels, loss_rows, lse, dlogits, ldd, M, V, loss, inv_count, ignore_index=-100):

@@ -72,6 +72,33 @@ __device__ __forceinline__ float xor_sum(float v) {
   auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
+// Sum over the 16 lanes of a DPP row (lanes with the same l >> 4): every lane gets the row total.
+__device__ __forceinline__ float row16_sum(float x) {
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xB1, 0xF, 0xF, false));   // quad_perm 1,0,3,2
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x4E, 0xF, 0xF, false));   // quad_perm 2,3,0,1
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x141, 0xF, 0xF, false));  // row_half_mirror
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x140, 0xF, 0xF, false));  // row_mirror
+  return x;
+}
+
+// Column sums of a wave's [32 rows][64 cols] output tile as stored (bf16-rounded), held as
+// v[grp][fd][r] = row 16grp + (l & 15), col 16fd + 4(l >> 4) + r. Returns lane l's share: the total of
+// column 16((l & 15) >> 2) + 4(l >> 4) + (l & 3), so one 64-lane store writes the tile's 64 sums.
+// (The qkv bias gradient: partial sums per 32 tokens, reduced over tokens by gpt2mi_colsum_f32.)
+__device__ __forceinline__ float tile_colsum(const f32x4 (&v)[2][4], float scale, int lane) {
+  const int j = lane & 15;
+  float mine = 0.f;
+#pragma unroll
+  for (int fd = 0; fd < 4; ++fd)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float t = row16_sum(bf2f(f2bf(v[0][fd][r] * scale)) + bf2f(f2bf(v[1][fd][r] * scale)));
+      mine = j == 4 * fd + r ? t : mine;
+    }
+  return mine;
+}
+__device__ __forceinline__ int tile_colsum_col(int lane) { return 16 * ((lane & 15) >> 2) + 4 * (lane >> 4) + (lane & 3); }
+
 constexpr float kRescaleThr = 8.f;  // log2 units: P <= 256 between rescales (bf16-exact exponent range)
 
 // pack accumulator registers acc[2kk + (j>>2)][j&3] (j = 0..7) to a bf16 operand fragment
@@ -284,8 +311,9 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const bf16* __
                                                                   const bf16* __restrict__ dout,
                                                                   const float* __restrict__ lse,
                                                                   float* __restrict__ delta,
-                                                                  bf16* __restrict__ dqkv, int T, int H, float scale,
-                                                                  uint64_t seed, uint32_t thr, float inv_keep) {
+                                                                  bf16* __restrict__ dqkv, float* __restrict__ csum,
+                                                                  int T, int H, float scale, uint64_t seed,
+                                                                  uint32_t thr, float inv_keep) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * BKV * 128];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
   const int nqb = (T + BQ - 1) / BQ;
@@ -418,6 +446,10 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const bf16* __
           bf16x4{f2bf(dq[qg][fd][0] * scale), f2bf(dq[qg][fd][1] * scale), f2bf(dq[qg][fd][2] * scale),
                  f2bf(dq[qg][fd][3] * scale)};
   }
+  if (csum) {  // partial qkv-bias gradient: row (b*T + q_lo)/32 of csum [B*T/32][3C], q columns
+    const float cs = tile_colsum(dq, scale, lane);
+    csum[((size_t)b * T + q_lo) / 32 * 3 * C + h * D + tile_colsum_col(lane)] = cs;
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -427,8 +459,9 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dkdv_kernel(const bf16* 
                                                                     const bf16* __restrict__ dout,
                                                                     const float* __restrict__ lse,
                                                                     const float* __restrict__ delta,
-                                                                    bf16* __restrict__ dqkv, int T, int H, float scale,
-                                                                    uint64_t seed, uint32_t thr, float inv_keep) {
+                                                                    bf16* __restrict__ dqkv, float* __restrict__ csum,
+                                                                    int T, int H, float scale, uint64_t seed,
+                                                                    uint32_t thr, float inv_keep) {
   constexpr int kTile = BQT * 128;
   constexpr int kStage = 2 * kTile + 2 * BQT * 4;
   __shared__ __attribute__((aligned(16))) char smem[2 * kStage];  // 2 x (Q, dO, lse, delta)
@@ -588,6 +621,13 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dkdv_kernel(const bf16* 
                  f2bf(dv[kg][fd][3] * vs)};
     }
   }
+  if (csum) {  // partial qkv-bias gradient: row (b*T + k_lo)/32 of csum [B*T/32][3C], k and v columns
+    float* crow = csum + ((size_t)b * T + k_lo) / 32 * 3 * C + C + h * D + tile_colsum_col(lane);
+    const float ck = tile_colsum(dk, scale, lane);
+    const float cv = tile_colsum(dv, DROP ? inv_keep : 1.f, lane);
+    crow[0] = ck;
+    crow[C] = cv;
+  }
 }
 
 }  // namespace
@@ -610,8 +650,8 @@ GPT2MI_EXPORT int gpt2mi_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse
 }
 
 GPT2MI_EXPORT int gpt2mi_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse,
-                                  float* delta, uint16_t* dqkv, int B, int T, int H, int head_dim, float p_drop,
-                                  uint64_t seed, void* stream) {
+                                  float* delta, uint16_t* dqkv, float* dqkv_colsum, int B, int T, int H,
+                                  int head_dim, float p_drop, uint64_t seed, void* stream) {
   GPT2MI_REQUIRE(head_dim == D, "attn_bwd: head_dim=%d (only 64 is built)", head_dim);
   GPT2MI_REQUIRE(T % 64 == 0 && T > 0, "attn_bwd: T=%d must be a multiple of 64", T);
   hipStream_t s = (hipStream_t)stream;
@@ -622,18 +662,18 @@ GPT2MI_EXPORT int gpt2mi_attn_bwd(const uint16_t* qkv, const uint16_t* out, cons
   const dim3 gq((T + BQ - 1) / BQ, B * H);
   if (thr)
     attn_bwd_dq_kernel<true><<<gq, kThreads, 0, s>>>((const bf16*)qkv, (const bf16*)out, (const bf16*)dout, lse, delta,
-                                                     (bf16*)dqkv, T, H, scale, seed, thr, ik);
+                                                     (bf16*)dqkv, dqkv_colsum, T, H, scale, seed, thr, ik);
   else
     attn_bwd_dq_kernel<false><<<gq, kThreads, 0, s>>>((const bf16*)qkv, (const bf16*)out, (const bf16*)dout, lse,
-                                                      delta, (bf16*)dqkv, T, H, scale, seed, thr, ik);
+                                                      delta, (bf16*)dqkv, dqkv_colsum, T, H, scale, seed, thr, ik);
   int rc = gpt2mi::check_launch("attn_bwd_dq");
   if (rc) return rc;
   const dim3 gkv((T + BKB - 1) / BKB, B * H);
   if (thr)
     attn_bwd_dkdv_kernel<true><<<gkv, kThreads, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta,
-                                                        (bf16*)dqkv, T, H, scale, seed, thr, ik);
+                                                        (bf16*)dqkv, dqkv_colsum, T, H, scale, seed, thr, ik);
   else
     attn_bwd_dkdv_kernel<false><<<gkv, kThreads, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta,
-                                                         (bf16*)dqkv, T, H, scale, seed, thr, ik);
+                                                         (bf16*)dqkv, dqkv_colsum, T, H, scale, seed, thr, ik);
   return gpt2mi::check_launch("attn_bwd_dkdv");
 }

@@ -433,9 +433,10 @@ GPT2MI_EXPORT int gpt2mi_attn_fwd_f32(const float* qkv, float* out, float* lse, 
 }
 
 GPT2MI_EXPORT int gpt2mi_attn_bwd_f32(const float* qkv, const float* out, const float* dout, const float* lse,
-                                      float* delta, float* dqkv, int B, int T, int H, int head_dim, float p_drop,
-                                      uint64_t seed, void* stream) {
+                                      float* delta, float* dqkv, float* dqkv_colsum, int B, int T, int H,
+                                      int head_dim, float p_drop, uint64_t seed, void* stream) {
   GPT2MI_REQUIRE(head_dim == HD, "attn_bwd_f32: head_dim=%d (only 64 is built)", head_dim);
+  GPT2MI_REQUIRE(dqkv_colsum == nullptr, "attn_bwd_f32: the fused bias-gradient partials are bf16-path only");
   GPT2MI_REQUIRE(T % RT == 0 && T > 0, "attn_bwd_f32: T=%d must be a multiple of 64", T);
   hipStream_t s = (hipStream_t)stream;
   const float scale = 1.f / sqrtf((float)head_dim);

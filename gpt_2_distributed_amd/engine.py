@@ -15,7 +15,7 @@ HBM layout per (B, T) workspace (M = B*T tokens, C = n_embd, Vp = vocab padded t
              lse fp32 [B*H,T]; x_mid fp32 [M,C]; gelu output h and dgelu = keep/(1-p)*gelu'(u) bf16 [M,4C]
   head:      ln_f bf16 [M,C]; logits bf16 [M,Vp] (returned as a [B,T,V] view); dlogits bf16 [M,Vp]
   backward scratch: dres fp32 [M,C], dres_bf bf16 [M,C], dln bf16 [M,C], dU bf16 [M,4C],
-             dqkv bf16 [M,3C], delta fp32 [B*H,T]
+             dqkv bf16 [M,3C], delta fp32 [B*H,T], dqkv_cs fp32 [M/32,3C]
 """
 from __future__ import annotations
 
@@ -87,6 +87,8 @@ class Workspace:
         self.dU = e(M, 4 * C)
         self.dqkv = e(M, 3 * C)
         self.delta = e(B * H, T, dt=F32)
+        # bf16 path: the attention backward writes 32-token partial column sums of dqkv (qkv bias grad)
+        self.dqkv_cs = e(M // 32, 3 * C, dt=F32) if act == BF16 else None
         # split-K slabs of the 256x256 wgrad GEMMs
         wshapes = [(3 * C, C), (C, C), (4 * C, C), (C, 4 * C), (vpad, C)]
         need = max((K_wgrad_splits(m, n, M) * m * n if K_wgrad_splits(m, n, M) > 1 else 0)
@@ -450,10 +452,14 @@ class Engine:
             # ---- attention
             dgrad(ws.dln, ws.dres_bf, pre + "attn.proj.weight", C, C)
             wgrad(C, C, ws.dres_bf, C, A.ao, C, self.g(pre + "attn.proj.weight"))
-            K.attn_bwd(A.qkv, A.ao, ws.dln, A.lse, ws.delta, ws.dqkv, B, T, H, C // H, pa, seeds[("attn", l)])
+            K.attn_bwd(A.qkv, A.ao, ws.dln, A.lse, ws.delta, ws.dqkv, B, T, H, C // H, pa, seeds[("attn", l)],
+                       colsum=ws.dqkv_cs)
             dgrad(ws.dln, ws.dqkv, pre + "attn.qkv.weight", C, 3 * C)
             wgrad(3 * C, C, ws.dqkv, 3 * C, A.ln1, C, self.g(pre + "attn.qkv.weight"))
-            K.colsum_bf16(ws.dqkv, self.g(pre + "attn.qkv.bias"), M, 3 * C, 3 * C)
+            if ws.dqkv_cs is not None:  # qkv bias grad: sum the attention backward's 32-token partials
+                K.colsum_bf16(ws.dqkv_cs, self.g(pre + "attn.qkv.bias"), M // 32, 3 * C, 3 * C)
+            else:
+                K.colsum_bf16(ws.dqkv, self.g(pre + "attn.qkv.bias"), M, 3 * C, 3 * C)
             if l > 0:
                 K.layernorm_bwd(x[l], self.p(pre + "ln1.weight"), A.m1, A.r1, ws.dln, ws.dres,
                                 self.g(pre + "ln1.weight"), self.g(pre + "ln1.bias"), ws.dres_bf,

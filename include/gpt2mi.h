@@ -78,9 +78,12 @@ int gpt2mi_gemm_wgrad(int M, int N, int K, const uint16_t* A, int lda, const uin
  * out [B*T, C] head-merged; lse [B*H, T] (natural log of the 1/sqrt(D)-scaled scores). */
 int gpt2mi_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int T, int H, int head_dim, float p_drop,
                     uint64_t seed, void* stream);
-/* Backward: delta [B*H, T] workspace; dqkv [B*T, 3C] written in the qkv layout. */
+/* Backward: delta [B*H, T] workspace (dO.O, formed by the dQ pass); dqkv [B*T, 3C] written in the qkv
+ * layout. dqkv_colsum (may be NULL): [B*T/32, 3C] fp32 partial column sums of the stored dqkv, one row
+ * per 32 tokens — the qkv bias gradient after gpt2mi_colsum_f32 over its rows (model.py c_attn bias). */
 int gpt2mi_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse, float* delta,
-                    uint16_t* dqkv, int B, int T, int H, int head_dim, float p_drop, uint64_t seed, void* stream);
+                    uint16_t* dqkv, float* dqkv_colsum, int B, int T, int H, int head_dim, float p_drop,
+                    uint64_t seed, void* stream);
 
 /* K13: F.cross_entropy(logits.view(-1,V), labels.view(-1), ignore_index) — model.py:357-359.
  * logits bf16 [M, ld]; writes loss_rows [M], lse [M], loss[0] = mean, inv_count[0] = 1/#valid and, if
@@ -112,7 +115,8 @@ int gpt2mi_gemm_f32(int layout, int epilogue, int M, int N, int K, const float* 
 int gpt2mi_attn_fwd_f32(const float* qkv, float* out, float* lse, int B, int T, int H, int head_dim, float p_drop,
                         uint64_t seed, void* stream);
 int gpt2mi_attn_bwd_f32(const float* qkv, const float* out, const float* dout, const float* lse, float* delta,
-                        float* dqkv, int B, int T, int H, int head_dim, float p_drop, uint64_t seed, void* stream);
+                        float* dqkv, float* dqkv_colsum /* must be NULL */, int B, int T, int H, int head_dim,
+                        float p_drop, uint64_t seed, void* stream);
 /* LayerNorm backward with fp32 dy and fp32 branch output (see gpt2mi_layernorm_bwd). */
 int gpt2mi_layernorm_bwd_f32(const float* x, const float* w, const float* mean, const float* rstd, const float* dy,
                              float* dres, float* dw, float* db, float* out_f32, float* dbias_out, int M, int C,

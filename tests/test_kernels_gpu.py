@@ -266,6 +266,32 @@ def test_attention_fwd_bwd(B, T, H):
     assert rel_err(dv, v.grad) < 1e-2
 
 
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_attention_bwd_fused_bias_grad_partials(p):
+    """The backward's 32-token partial column sums of the stored dqkv (the qkv bias gradient, summed by
+    colsum) equal the column sums of dqkv itself, and requesting them leaves dqkv unchanged."""
+    B, T, H, D = 2, 256, 4, 64
+    qkv, C = _attn_inputs(B, T, H, 77)
+    qd = qkv.to(dev)
+    out = torch.empty(B * T, C, dtype=torch.bfloat16, device=dev)
+    lse = torch.empty(B * H, T, device=dev)
+    L().attn_fwd(qd, out, lse, B, T, H, D, p, 5)
+    dout = bf(torch.randn(B * T, C, generator=torch.Generator().manual_seed(1))).to(dev)
+    delta = torch.empty(B * H, T, device=dev)
+    d1 = torch.empty(B * T, 3 * C, dtype=torch.bfloat16, device=dev)
+    d2 = torch.empty_like(d1)
+    cs = torch.empty(B * T // 32, 3 * C, device=dev)
+    L().attn_bwd(qd, out, dout, lse, delta, d1, B, T, H, D, p, 5)
+    L().attn_bwd(qd, out, dout, lse, delta, d2, B, T, H, D, p, 5, colsum=cs)
+    torch.cuda.synchronize()
+    assert torch.equal(d1, d2)
+    ref = d1.float().view(B * T // 32, 32, 3 * C).sum(1)
+    assert rel_err(cs.cpu(), ref.cpu()) < 1e-5
+    bias_grad = torch.zeros(3 * C, device=dev)
+    L().colsum_bf16(cs, bias_grad, B * T // 32, 3 * C, 3 * C)
+    assert rel_err(bias_grad.cpu(), d1.float().sum(0).cpu()) < 1e-5
+
+
 def test_attention_dropout_stats_and_grad_consistency():
     """With p>0 the expected output equals the no-dropout output; the backward regenerates the
     same mask (checked through a finite-difference-free identity: <dO, O> = <dV, V> at fixed P)."""
