@@ -419,8 +419,11 @@ template <typename TG>
 static int colsum_t(const TG* g, float* db, int M, int N, int ld, void* stream) {
   GPT2MI_REQUIRE(N % 4 == 0 && ld % 4 == 0, "colsum: N=%d and ld=%d must be multiples of 4", N, ld);
   hipStream_t s = (hipStream_t)stream;
-  const int rpb = 256;
-  dim3 grid((N + 255) / 256, (M + rpb - 1) / rpb);
+  // >= ~1024 blocks (the 32-token partial sums of the attention backward are only M/32 rows)
+  const int gx = (N + 255) / 256;
+  const int want_y = (1024 + gx - 1) / gx;
+  const int rpb = std::max(8, std::min(256, (M + want_y - 1) / want_y));
+  dim3 grid(gx, (M + rpb - 1) / rpb);
   colsum_kernel<TG><<<grid, 256, 0, s>>>(g, db, M, N, ld, rpb);
   return gpt2mi::check_launch("colsum");
 }
