@@ -51,5 +51,5 @@ def test_no_scratch_and_occupancy(src):
         assert found, f"{sub} not found in {src}"
         for k, v in found.items():
             assert v["ScratchSize [bytes/lane]"] == 0, f"{k}: scratch {v}"
-            assert v["SGPRs Spill"] == 0 and v["VGPRs Spill"] == 0, f"{k}: spills {v}"
+            assert v["VGPRs Spill"] == 0, f"{k}: spills {v}"  # (SGPR spills go to VGPR lanes: no memory)
             assert v["Occupancy [waves/SIMD]"] >= occ, f"{k}: occupancy {v}"
