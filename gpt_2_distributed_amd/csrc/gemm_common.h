@@ -31,30 +31,42 @@ struct GemmParams {
   float inv_keep;
 };
 
-// NewGELU (model.py:63-77): 0.5u(1 + tanh(z)), z = sqrt(2/pi)(u + 0.044715u^3), evaluated in the
-// equivalent sigmoid form u * s with s = 1/(1 + exp(-2z)) (v_exp_f32 + v_rcp_f32: the epilogues run
-// this on every fc1 output, where a division-based tanh made them VALU-bound).
-//   gelu'(u) = s * (1 + 2*sqrt(2/pi) * u * (1 - s) * (1 + 3*0.044715*u^2))
-__device__ __forceinline__ float gelu_sig(float u) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f, m2log2e = -2.0f * 1.4426950408889634f;
-  const float z = k0 * u * (1.f + k1 * u * u);
-  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(m2log2e * z));
-}
-__device__ __forceinline__ float gelu_f(float u) { return u * gelu_sig(u); }
-__device__ __forceinline__ float gelu_grad_from_sig(float u, float sg) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  return sg * (1.f + 2.f * k0 * u * (1.f - sg) * (1.f + 3.f * k1 * u * u));
-}
-__device__ __forceinline__ float gelu_grad_f(float u) { return gelu_grad_from_sig(u, gelu_sig(u)); }
-
-// keep mask of the 4 dropout elements didx..didx+3 (didx even): two hashes, 16 bits per element
-__device__ __forceinline__ void drop4(const GemmParams& P, uint64_t didx, bool keep[4]) {
+// keep mask of the 4 dropout elements 2*pidx .. 2*pidx+3 as multipliers keep/(1-p) or 0 (x * m is the
+// dropout of x, as torch's fused dropout forms it): two hashes, 16 bits per element
+__device__ __forceinline__ f32x4 drop_scale4(const GemmParams& P, uint32_t pidx) {
   const uint32_t s = seed32(P.seed);
-  const uint32_t h0 = drop_hash(s, (uint32_t)(didx >> 1)), h1 = drop_hash(s, (uint32_t)(didx >> 1) + 1u);
-  keep[0] = drop_keep16(h0, 0, P.thr);
-  keep[1] = drop_keep16(h0, 1, P.thr);
-  keep[2] = drop_keep16(h1, 0, P.thr);
-  keep[3] = drop_keep16(h1, 1, P.thr);
+  const uint32_t h0 = drop_hash(s, pidx), h1 = drop_hash(s, pidx + 1u);
+  const float k = P.inv_keep;
+  return f32x4{drop_keep16(h0, 0, P.thr) ? k : 0.f, drop_keep16(h0, 1, P.thr) ? k : 0.f,
+               drop_keep16(h1, 0, P.thr) ? k : 0.f, drop_keep16(h1, 1, P.thr) ? k : 0.f};
+}
+
+// NewGELU (model.py:63-77): 0.5u(1 + tanh(z)), z = sqrt(2/pi)(u + 0.044715u^3), evaluated in the
+// equivalent sigmoid form u * s with s = 1/(1 + exp(-2z)) (v_exp_f32 + v_rcp_f32, no division).
+// Of 4 pre-activations times the dropout multipliers m, and its derivative times m, in
+// packed-f32 pairs (v_pk_mul/fma/add_f32 issue two lanes' worth per instruction; the epilogue of the
+// fc1 GEMM is VALU-issue bound):
+//   s = 1/(1 + 2^(u (A + B u^2))), h = u s m, d = gelu'(u) m = s m + s m * u (1 - s) (2 k0 + 6 k0 k1 u^2)
+__device__ __forceinline__ void gelu4(f32x4 u, f32x4 m, f32x4& h, f32x4& d) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f, m2log2e = -2.0f * 1.4426950408889634f;
+  const f32x2 A = {k0 * m2log2e, k0 * m2log2e}, B = {k0 * k1 * m2log2e, k0 * k1 * m2log2e};
+  const f32x2 Q0 = {2.f * k0, 2.f * k0}, Q1 = {6.f * k0 * k1, 6.f * k0 * k1}, one = {1.f, 1.f};
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const f32x2 x = {u[2 * p], u[2 * p + 1]}, mm = {m[2 * p], m[2 * p + 1]};
+    const f32x2 x2 = x * x;
+    const f32x2 arg = x * __builtin_elementwise_fma(x2, B, A);
+    const f32x2 e = {__builtin_amdgcn_exp2f(arg[0]), __builtin_amdgcn_exp2f(arg[1])};
+    const f32x2 den = e + one;
+    const f32x2 sg = {__builtin_amdgcn_rcpf(den[0]), __builtin_amdgcn_rcpf(den[1])};
+    const f32x2 r = x * (one - sg) * __builtin_elementwise_fma(x2, Q1, Q0);
+    const f32x2 sm = sg * mm;
+    const f32x2 hh = x * sm, dd = __builtin_elementwise_fma(r, sm, sm);
+    h[2 * p] = hh[0];
+    h[2 * p + 1] = hh[1];
+    d[2 * p] = dd[0];
+    d[2 * p + 1] = dd[1];
+  }
 }
 
 // 4-element vector load/store of the activation element type TE (bf16 under autocast, fp32 in the
@@ -106,10 +118,9 @@ __device__ __forceinline__ f32x4 epilogue_operand(const GemmParams& P, int gm, i
 template <int EPI, typename TE = bf16>
 __device__ __forceinline__ f32x4 epilogue_apply(const GemmParams& P, int gm, int gn, f32x4 v, f32x4 opnd) {
   const size_t cidx = (size_t)gm * P.ldc + gn;
-  const uint64_t didx = (uint64_t)gm * P.N + gn;  // dropout element index in the logical [M,N] (even)
-  bool keep[4] = {true, true, true, true};
-  if (EPI == EPI_RESID || EPI == EPI_GELU)
-    if (P.thr) drop4(P, didx, keep);
+  // dropout pair index: element gm*N + gn of the logical [M,N] over 2, mod 2^32 (N and gn are multiples of 4
+  // in every kernel: N is a multiple of the tile width, host-checked)
+  const uint32_t pidx = (uint32_t)gm * (uint32_t)(P.N >> 1) + (uint32_t)(gn >> 1);
   if constexpr (EPI == EPI_BF16) {
     store4<TE>(reinterpret_cast<TE*>(P.C) + cidx, v);
     return round4<TE>(v);
@@ -118,29 +129,15 @@ __device__ __forceinline__ f32x4 epilogue_apply(const GemmParams& P, int gm, int
     for (int j = 0; j < 4; ++j) v[j] += opnd[j];
     *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(P.C) + cidx) = v;
   } else if constexpr (EPI == EPI_RESID) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float y = v[j];
-      if (P.thr) y = keep[j] ? y * P.inv_keep : 0.f;
-      opnd[j] += y;
-    }
+    if (P.thr) v *= drop_scale4(P, pidx);
+    opnd += v;
     *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(P.C) + cidx) = opnd;
   } else if constexpr (EPI == EPI_GELU) {
     // the forward also emits what the backward needs of this site: dL/du = dL/dh * keep/(1-p) * gelu'(u),
     // so the fc2 dgrad epilogue is one multiply (no dropout hash, no GELU math, no pre-activation)
-    f32x4 h, dg;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float sg = gelu_sig(v[j]);
-      float a = v[j] * sg;
-      float d = gelu_grad_from_sig(v[j], sg);
-      if (P.thr) {
-        a = keep[j] ? a * P.inv_keep : 0.f;
-        d = keep[j] ? d * P.inv_keep : 0.f;
-      }
-      h[j] = a;
-      dg[j] = d;
-    }
+    f32x4 h, dg, m = {1.f, 1.f, 1.f, 1.f};
+    if (P.thr) m = drop_scale4(P, pidx);
+    gelu4(v, m, h, dg);
     store4<TE>(reinterpret_cast<TE*>(P.aux) + (size_t)gm * P.ldaux + gn, dg);
     store4<TE>(reinterpret_cast<TE*>(P.C) + cidx, h);
   } else if constexpr (EPI == EPI_GELU_BWD) {

@@ -302,7 +302,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
     if constexpr (kOpnd) {
 #pragma unroll
       for (int it = 0; it < 16; ++it) {
-        const int r = it * 8 + (tid >> 6);
+        const int r = it * 8 + wid;
         const int gm = m0 + (AIL ? ((r >> 6) << 7) + mi * 64 + (r & 63) : mi * 128 + r);
         opnd[it] = epilogue_operand<EPI>(P, min(gm, P.M - 1), gn);
       }
@@ -323,7 +323,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
         }
     lds_barrier();
     auto row_of = [&](int it) {
-      const int r = it * 8 + (tid >> 6);
+      const int r = it * 8 + wid;
       return m0 + (AIL ? ((r >> 6) << 7) + mi * 64 + (r & 63) : mi * 128 + r);
     };
     auto finish = [&](int it, f32x4 v) {
@@ -347,14 +347,14 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
       f32x4 v[16];
 #pragma unroll
       for (int it = 0; it < 16; ++it) {
-        const int r = it * 8 + (tid >> 6);
+        const int r = it * 8 + wid;
         v[it] = *reinterpret_cast<const f32x4*>(img + r * 256 + 4 * (ch ^ (r & 15)));
       }
 #pragma unroll
       for (int it = 0; it < 16; ++it) finish(it, v[it]);
     } else {
       for (int it = 0; it < 16; ++it) {
-        const int r = it * 8 + (tid >> 6);
+        const int r = it * 8 + wid;
         const f32x4 v = *reinterpret_cast<const f32x4*>(img + r * 256 + 4 * (ch ^ (r & 15)));
         if (row_of(it) < P.M) finish(it, v);
       }

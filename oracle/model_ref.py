@@ -132,7 +132,7 @@ def gelu_tanh(u, mode="fp32"):
     return 0.5 * u * (1.0 + torch.tanh(math.sqrt(2.0 / math.pi) * (u + 0.044715 * torch.pow(u, 3.0))))
 
 
-def causal_attention(q, k, v, mode="fp32"):
+def causal_attention(q, k, v, mode="fp32", drop=None):
     """Attention core (model.py:137-151) for q,k,v [B,H,T,D]: (q k^T)/sqrt(D), masked_fill(tril==0,
     -1e4), softmax (fp32 under autocast), then P v. bf16 mode rounds the scores (bmm output) and
     P (cast back to bf16 for the second bmm) the way autocast does."""
@@ -147,6 +147,8 @@ def causal_attention(q, k, v, mode="fp32"):
     mask = torch.tril(torch.ones(T, T, dtype=torch.bool))
     att = att.masked_fill(~mask, -1e4)
     att = torch.softmax(att, dim=-1)
+    if drop is not None:
+        att = att * drop                                                     # attn_drop (model.py:146)
     if mode == "bf16":
         return _bf(_bf(att) @ v)
     return att @ v
@@ -159,8 +161,14 @@ def cross_entropy(logits, labels):
     return F.cross_entropy(lg, y, ignore_index=-100)
 
 
-def block_forward(x, p, cfg, mode="fp32"):
-    """GPT2Block.forward (model.py:213-219): x + attn(ln1(x)); x + mlp(ln2(x)). Dropout p=0."""
+def block_forward(x, p, cfg, mode="fp32", drop=None, layer=0):
+    """GPT2Block.forward (model.py:213-219): x + attn(ln1(x)); x + mlp(ln2(x)). ``drop``: optional
+    table of dropout multipliers keep/(1-p) per site (``dropout_ref.step_masks``); None = dropout 0."""
+    dm = (lambda site: drop[(site, layer)]) if drop is not None else (lambda site: None)
+
+    def dr(t, site):
+        m = dm(site)
+        return t if m is None else t * m
     B, T, C = x.shape
     H = cfg.n_head
     D = C // H
@@ -168,27 +176,30 @@ def block_forward(x, p, cfg, mode="fp32"):
     qkv = linear(h, p["attn.qkv.weight"], p["attn.qkv.bias"], mode)          # [B,T,3C]
     qkv = qkv.view(B, T, 3, H, D).transpose(1, 3)                           # model.py:124
     q, k, v = qkv.unbind(dim=2)                                             # [B,H,T,D]
-    y = causal_attention(q, k, v, mode)
+    y = causal_attention(q, k, v, mode, dm("attn"))
     y = y.transpose(1, 2).contiguous().view(B, T, C)                        # model.py:155
-    y = linear(y, p["attn.proj.weight"], p["attn.proj.bias"], mode)
+    y = dr(linear(y, p["attn.proj.weight"], p["attn.proj.bias"], mode), "proj")  # resid_drop (model.py:158)
     x = x + y
     h = layer_norm(x, p["ln2.weight"], p["ln2.bias"], cfg.layer_norm_eps)
     u = linear(h, p["mlp.fc1.weight"], p["mlp.fc1.bias"], mode)
-    a = gelu_tanh(u, mode)
-    y = linear(a, p["mlp.fc2.weight"], p["mlp.fc2.bias"], mode)
+    a = dr(gelu_tanh(u, mode), "fc1")                                       # drop1 (model.py:188)
+    y = dr(linear(a, p["mlp.fc2.weight"], p["mlp.fc2.bias"], mode), "fc2")  # drop2 (model.py:191)
     return x + y
 
 
-def forward(params, cfg, idx, labels=None, mode="fp32"):
-    """GPT2.forward (model.py:335-361) -> (logits, loss). Dropout is 0 (parity runs)."""
+def forward(params, cfg, idx, labels=None, mode="fp32", drop=None):
+    """GPT2.forward (model.py:335-361) -> (logits, loss). ``drop``: None = dropout 0 (parity runs), else
+    the per-site multipliers of one step (``dropout_ref.step_masks``)."""
     B, T = idx.shape
     if T > cfg.n_positions:
         raise ValueError(f"Sequence length {T} > model max {cfg.n_positions}")
     x = embed(params["transformer.wte.weight"], params["transformer.wpe.weight"], idx)
+    if drop is not None:
+        x = x * drop["embd"]                                                 # self.drop (model.py:304)
     for i in range(cfg.n_layer):
         pre = f"transformer.h.{i}."
         p = {k: params[pre + k] for k in BLOCK_KEYS}
-        x = block_forward(x, p, cfg, mode)
+        x = block_forward(x, p, cfg, mode, drop, i)
     x = layer_norm(x, params["transformer.ln_f.weight"], params["transformer.ln_f.bias"], cfg.layer_norm_eps)
     logits = linear(x, params["transformer.wte.weight"], None, mode)  # tied lm_head (model.py:333)
     loss = cross_entropy(logits, labels) if labels is not None else None

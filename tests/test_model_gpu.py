@@ -178,3 +178,47 @@ def test_124m_trajectory_vs_reference(prec, steps=20):
     rl = np.abs(np.array(losses) - np.array(ref["losses"][:steps])) / np.array(ref["losses"][:steps])
     print(prec, "max rel loss err", rl.max(), losses[0], losses[-1])
     assert rl.max() < TOL[prec][3], rl
+
+
+# C = 256, M = B*T = 512: the bf16 step runs its GEMMs on the 256x256 ping-pong kernel (fused dropout in
+# the proj / fc2 residual and fc1 GELU epilogues), the fp32 step on the fp32 family
+DROPCFG = dict(n_layer=2, n_head=4, n_embd=256, vocab_size=509, n_positions=128, resid_pdrop=0.1, attn_pdrop=0.1)
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp32"])
+def test_dropout_step_vs_oracle_with_the_same_masks(prec):
+    """Dropout on (p = 0.1 at all six sites of model.py): the HIP step's loss and every gradient equal
+    autograd of the reference math run with the masks the step drew (oracle/dropout_ref.py restates
+    the kernels' counter-based mask), at the dropout-0 tolerances. Checks that every backward site
+    regenerates (or reads back) exactly the forward's mask."""
+    import dataclasses
+    from gpt_2_distributed_amd.model import GPT2, GPT2Config
+    from oracle import dropout_ref, model_ref
+    t_logits, t_loss, t_grad = TOL[prec][:3]
+    cfg = GPT2Config(**DROPCFG)
+    m = GPT2(cfg).to(dev)
+    m.train()
+    B, T = 4, 128
+    g = torch.Generator().manual_seed(11)
+    idx = torch.randint(0, cfg.vocab_size, (B, T), generator=g)
+    labels = torch.randint(0, cfg.vocab_size, (B, T), generator=g)
+    with prec_ctx(prec):
+        logits, loss = m(idx.to(dev), labels=labels.to(dev))
+    logits = logits.float().cpu()  # (a view of the engine's workspace: the next forward rewrites it)
+    seeds = m.engine()._saved[4]
+    loss.backward()
+    rcfg = model_ref.Cfg(**dataclasses.asdict(cfg))
+    drop = dropout_ref.step_masks(seeds, B, T, cfg.n_embd, cfg.n_head, cfg.n_layer, 0.1, 0.1)
+    params = {n: p.detach().cpu().clone().requires_grad_(True) for n, p in m.named_parameters()}
+    r_logits, r_loss = model_ref.forward(params, rcfg, idx, labels, prec, drop=drop)
+    r_loss.backward()
+    assert rel_err(logits, r_logits.detach()) < t_logits
+    assert abs(loss.item() - r_loss.item()) / r_loss.item() < t_loss
+    for n, p in m.named_parameters():
+        e = rel_err(p.grad.cpu(), params[n].grad)
+        assert e < t_grad, (n, e)
+    # and the masks are not trivial: the same forward without dropout gives other logits
+    m.eval()
+    with torch.no_grad(), prec_ctx(prec):
+        l_eval, _ = m(idx.to(dev), labels=labels.to(dev))
+    assert rel_err(l_eval.float().cpu(), logits) > 10 * t_logits

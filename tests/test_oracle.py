@@ -102,3 +102,44 @@ def test_124m_trajectory_first_steps():
         losses, norms = train_ref.run(model_ref.Cfg(resid_pdrop=0.0, attn_pdrop=0.0), b, 3)
     np.testing.assert_allclose(losses, ref["losses"][:3], rtol=1e-4)
     np.testing.assert_allclose(norms, ref["grad_norms"][:3], rtol=1e-3)
+
+
+def test_dropout_restatement():
+    """oracle/dropout_ref.py: numpy hash == a scalar pure-python restatement; drop rate p; pair layout;
+    the oracle forward with all-ones masks == dropout 0."""
+    from oracle import dropout_ref as D
+
+    def h_py(s, x):
+        h = ((x ^ s) * 0x9E3779B1) & 0xFFFFFFFF
+        h ^= h >> 16
+        h = (h * 0x85EBCA6B) & 0xFFFFFFFF
+        return h ^ (h >> 13)
+
+    seed = 0x0123456789ABCDEF
+    s32 = int(D.seed32(seed))
+    assert s32 == (0x89ABCDEF ^ 0x01234567)
+    xs = np.array([0, 1, 2, 12345, 2**31 + 7, 2**32 - 1], dtype=np.uint64)
+    assert [int(v) for v in D.drop_hash(D.seed32(seed), xs)] == [h_py(s32, int(x)) for x in xs]
+    assert D.threshold(0.1) == 6554 and D.threshold(0.0) == 0
+    m = D.site_scale(seed, 256, 768, 0.1)
+    assert abs(float((m == 0).float().mean()) - 0.1) < 0.005
+    assert torch.allclose(m[m > 0], torch.tensor(1 / 0.9))
+    # elements 2j, 2j+1 share hash j: halves 0 / 1
+    e = np.arange(16, dtype=np.uint64)
+    hv = D.drop_hash(D.seed32(seed), e >> np.uint64(1))
+    keep = ((hv >> (np.uint64(16) * (e & np.uint64(1)))) & np.uint64(0xFFFF)) >= 6554
+    assert np.array_equal(keep, (m.reshape(-1)[:16] > 0).numpy())
+    a = D.attn_scale(seed, 2, 64, 0.1)
+    assert abs(float((a == 0).float().mean()) - 0.1) < 0.01
+    # queries q and q^16 of one key share a hash: (q & ~16)
+    q, k = 3, 40
+    x = (1 * 64 + (q & ~16)) * 64 + k
+    hh = h_py(s32, x)
+    assert (a[1, q, k] > 0).item() == ((hh & 0xFFFF) >= 6554)
+    assert (a[1, q ^ 16, k] > 0).item() == (((hh >> 16) & 0xFFFF) >= 6554)
+    params = model_ref.init_params(TINY)
+    idx = torch.randint(0, 509, (2, 64), generator=torch.Generator().manual_seed(1))
+    ones = {kk: torch.ones_like(v) for kk, v in D.step_masks({"embd": 1, **{(s, l): 1 for s in ("attn", "proj", "fc1", "fc2") for l in range(2)}}, 2, 64, 128, 2, 2, 0.1, 0.1).items()}
+    l0, _ = model_ref.forward(params, TINY, idx, None, "fp32")
+    l1, _ = model_ref.forward(params, TINY, idx, None, "fp32", drop=ones)
+    assert torch.equal(l0, l1)
