@@ -64,8 +64,9 @@ struct Loader {
       const bf16* p;
       if constexpr (!TRANS) {
         p = src + (size_t)min(row0 + id / 8, rmax) * ld + k0 + 8 * (id % 8);
-      } else {
-        p = src + (size_t)(k0 + id / (ROWS / 8)) * ld + row0 + 8 * (id % (ROWS / 8));
+      } else {  // partial last tile (extent % 128 == 64): clamp the 8-column chunk into the row (rmax+1 is a
+                // multiple of 64); the clamped columns only feed outputs the epilogue discards
+        p = src + (size_t)(k0 + id / (ROWS / 8)) * ld + min(row0 + 8 * (id % (ROWS / 8)), rmax - 7);
       }
       r[i] = *reinterpret_cast<const u32x4*>(p);
     }
@@ -93,7 +94,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams P) {
   const int wm = wid >> 1, wn = wid & 1;
 
   // tile scheduling: XCD-contiguous ranges, grouped-M ordering for L2 reuse
-  const int tiles_m = (P.M + BM - 1) / BM, tiles_n = P.N / BN;
+  const int tiles_m = (P.M + BM - 1) / BM, tiles_n = (P.N + BN - 1) / BN;
   const int ntiles = tiles_m * tiles_n;
   const int pid = xcd_remap(blockIdx.x, ntiles);
   constexpr int GM = 8;
@@ -175,7 +176,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams P) {
     for (int it = 0; it < (BM * BN) / kThreads; ++it) {
       const int id = threadIdx.x + kThreads * it;
       const int row = id / BN, col = id % BN;
-      if (m0 + row >= P.M) continue;
+      if (m0 + row >= P.M || n0 + col >= P.N) continue;
       atomicAdd(C + (size_t)(m0 + row) * P.ldc + n0 + col, alpha * ep[row * kEpiLd + col]);
     }
     return;
@@ -185,7 +186,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams P) {
       const int id = threadIdx.x + kThreads * it;
       const int row = id / (BN / 4), c4 = 4 * (id % (BN / 4));
       const int gm = m0 + row, gn = n0 + c4;
-      if (gm >= P.M) continue;
+      if (gm >= P.M || gn >= P.N) continue;
       f32x4 v = *reinterpret_cast<const f32x4*>(ep + row * kEpiLd + c4);
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[j] *= alpha;
@@ -201,7 +202,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams P) {
 
 template <bool A_T, bool B_T, int EPI>
 int launch(const GemmParams& P, int splits, hipStream_t s) {
-  dim3 grid(((P.M + BM - 1) / BM) * (P.N / BN), 1, splits);
+  dim3 grid(((P.M + BM - 1) / BM) * ((P.N + BN - 1) / BN), 1, splits);
   gemm_kernel<A_T, B_T, EPI><<<grid, kThreads, 0, s>>>(P);
   return gpt2mi::check_launch("gemm");
 }
@@ -220,8 +221,9 @@ GPT2MI_EXPORT int gpt2mi_gemm(int layout, int epilogue, int M, int N, int K, con
                               int splits, float p_drop, uint64_t seed, float* dbias, void* stream) {
   GPT2MI_REQUIRE(dbias == nullptr || ((epilogue == EPI_BF16 || epilogue == EPI_GELU_BWD) && layout <= 1),
                  "gemm: dbias (fused column sum) needs the BF16 or GELU_BWD epilogue of layout 0/1");
-  GPT2MI_REQUIRE(N % BN == 0 && M % 64 == 0 && M > 0, "gemm: N=%d must be a multiple of %d and M=%d of 64", N, BN, M);
-  GPT2MI_REQUIRE(layout != 2 || M % BM == 0, "gemm: wgrad needs M=%d a multiple of %d", M, BM);
+  // 128-wide tiles with a half-width last tile in N (and in M for the transposed A of wgrad): C = 1600
+  // (GPT-2 1.5B) gives N = 1600 / 4800
+  GPT2MI_REQUIRE(N % 64 == 0 && N > 0 && M % 64 == 0 && M > 0, "gemm: N=%d and M=%d must be multiples of 64", N, M);
   GPT2MI_REQUIRE(splits >= 1 && K % (BK * splits) == 0, "gemm: K=%d must be a multiple of %d*splits(%d)", K, BK,
                  splits);
   GPT2MI_REQUIRE(splits == 1 || epilogue == EPI_ATOMIC, "gemm: split-K needs the atomic epilogue");

@@ -126,7 +126,9 @@ def _gemm_ref(layout, A, B):
 
 
 @pytest.mark.parametrize("layout", [0, 1, 2])
-@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (256, 384, 768), (512, 256, 192)])
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (256, 384, 768), (512, 256, 192),
+                                   # half-width last tiles (C = 1600 of GPT-2 1.5B: N = 1600, 4800)
+                                   (192, 192, 128), (320, 576, 192)])
 def test_gemm_layouts_f32(layout, M, N, K):
     g = torch.Generator().manual_seed(M * 7 + N + K + layout)
     if layout == 0:
@@ -204,10 +206,37 @@ def test_gemm_gelu_bwd_dgrad():
 def test_gemm_rejects_bad_shapes():
     from gpt_2_distributed_amd._lib import KernelError
     A = torch.zeros(128, 128, dtype=torch.bfloat16, device=dev)
-    with pytest.raises(KernelError, match="multiple of 128"):
+    with pytest.raises(KernelError, match="multiples of 64"):
         L().gemm(0, 0, 128, 100, 64, A, 128, A, 128, A, 128)
     with pytest.raises(KernelError, match="of 64"):
         L().gemm(0, 0, 100, 128, 64, A, 128, A, 128, A, 128)
+
+
+def test_gemm_half_width_n_tile_epilogues():
+    """N % 128 == 64 (GPT-2 1.5B widths) on the 128x128 kernel: bias / GELU+dropout / residual epilogues
+    write exactly the N valid columns (the padding columns of a wider C stay untouched)."""
+    M, N, K = 256, 320, 192
+    g = torch.Generator().manual_seed(21)
+    A, W = bf(torch.randn(M, K, generator=g)), bf(torch.randn(N, K, generator=g) * 0.1)
+    bias, resid = torch.randn(N, generator=g), torch.randn(M, N, generator=g)
+    acc = A.float() @ W.float().t() + bias
+    Ad, Wd = A.to(dev), W.to(dev)
+    ld = N + 64
+    C = torch.full((M, ld), 3.0, dtype=torch.bfloat16, device=dev)
+    L().gemm(0, L().EPI_BF16, M, N, K, Ad, K, Wd, K, C, ld, bias=bias.to(dev))
+    assert rel_err(C[:, :N].cpu().float(), acc) < 4e-3
+    assert torch.all(C[:, N:] == 3.0)
+    Cr = torch.full((M, ld), 5.0, device=dev)
+    Rd = torch.zeros(M, ld, device=dev)
+    Rd[:, :N] = resid.to(dev)
+    L().gemm(0, L().EPI_RESID, M, N, K, Ad, K, Wd, K, Cr, ld, bias=bias.to(dev), resid=Rd)
+    assert rel_err(Cr[:, :N].cpu(), resid + acc) < 1e-5
+    assert torch.all(Cr[:, N:] == 5.0)
+    H = torch.full((M, ld), 3.0, dtype=torch.bfloat16, device=dev)
+    G = torch.full((M, ld), 3.0, dtype=torch.bfloat16, device=dev)
+    L().gemm(0, L().EPI_GELU, M, N, K, Ad, K, Wd, K, H, ld, bias=bias.to(dev), aux=G, ldaux=ld)
+    assert rel_err(H[:, :N].cpu().float(), model_ref.gelu_tanh(acc)) < 4e-3
+    assert torch.all(H[:, N:] == 3.0) and torch.all(G[:, N:] == 3.0)
 
 
 def test_gemm_partial_m_tile():

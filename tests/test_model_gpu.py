@@ -222,3 +222,32 @@ def test_dropout_step_vs_oracle_with_the_same_masks(prec):
     with torch.no_grad(), prec_ctx(prec):
         l_eval, _ = m(idx.to(dev), labels=labels.to(dev))
     assert rel_err(l_eval.float().cpu(), logits) > 10 * t_logits
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp32"])
+def test_non_256_width_model_vs_oracle(prec):
+    """Widths that are not multiples of 128/256, like GPT-2 1.5B (C = 1600, H = 25): here C = 192, H = 3
+    (3C = 576 and C take the half-width-tile path of the 128x128 GEMM, 4C = 768 the ping-pong kernel),
+    one step's loss and every gradient vs autograd of the oracle (dropout 0)."""
+    import dataclasses
+    from gpt_2_distributed_amd.model import GPT2, GPT2Config
+    from oracle import model_ref
+    t_logits, t_loss, t_grad = TOL[prec][:3]
+    cfg = GPT2Config(n_layer=2, n_head=3, n_embd=192, vocab_size=509, n_positions=64, resid_pdrop=0.0,
+                     attn_pdrop=0.0)
+    m = GPT2(cfg).to(dev)
+    g = torch.Generator().manual_seed(12)
+    idx = torch.randint(0, cfg.vocab_size, (4, 64), generator=g)
+    labels = torch.randint(0, cfg.vocab_size, (4, 64), generator=g)
+    with prec_ctx(prec):
+        logits, loss = m(idx.to(dev), labels=labels.to(dev))
+    logits = logits.float().cpu()
+    loss.backward()
+    params = {n: p.detach().cpu().clone().requires_grad_(True) for n, p in m.named_parameters()}
+    r_logits, r_loss = model_ref.forward(params, model_ref.Cfg(**dataclasses.asdict(cfg)), idx, labels, prec)
+    r_loss.backward()
+    assert rel_err(logits, r_logits.detach()) < t_logits
+    assert abs(loss.item() - r_loss.item()) / r_loss.item() < t_loss
+    for n, p in m.named_parameters():
+        e = rel_err(p.grad.cpu(), params[n].grad)
+        assert e < t_grad, (n, e)
