@@ -211,7 +211,6 @@ class ShardedDataParallel(DistributedDataParallel):
         super().__init__(module, device_ids, bucket_mb)
         W = dist.get_world_size()
         total = module.layout.total
-        assert total % W == 0 or True
         per = (total + W - 1) // W
         per = (per + 63) // 64 * 64
         self.per = per
@@ -226,7 +225,6 @@ class ShardedDataParallel(DistributedDataParallel):
         g = eng.grad
         if g.numel() < self.padded:
             raise RuntimeError("arena must be padded to the shard grid")
-        out = g[self.lo:self.lo + self.per] if self.hi - self.lo == self.per else None
         inp = g[:self.padded]
         shard = torch.empty(self.per, dtype=g.dtype, device=g.device)
         op = dist.ReduceOp.AVG if dist.get_backend() == "nccl" else dist.ReduceOp.SUM
@@ -247,6 +245,11 @@ class _ShardedOptimizer(_SyncedOptimizer):
     def step(self, closure=None):
         self.ddp.finish_gradient_sync()
         out = self.opt.step(closure)
+        # the kernel's norm covers this rank's slice: the clip_grad_norm_ value is the global one
+        # (train_gpt2_distributed.py:419-421 on the full grads)
+        n2 = self.opt.grad_norm.square()
+        dist.all_reduce(n2)
+        self.opt.grad_norm.copy_(n2.sqrt())
         # all-gather the updated fp32 master slices, then refresh the bf16 shadow once
         m = self.ddp.module
         arena = m.arena

@@ -15,13 +15,14 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 WORKER = r"""
 import os, sys, json, torch, torch.distributed as dist
 sys.path.insert(0, os.environ["REPO"])
-from gpt_2_distributed_amd.parallel import init_distributed, DistributedDataParallel
+from gpt_2_distributed_amd.parallel import init_distributed, DistributedDataParallel, ShardedDataParallel
 from gpt_2_distributed_amd.model import GPT2, GPT2Config
 init_distributed()
 r, w = dist.get_rank(), dist.get_world_size()
 cfg = GPT2Config(n_layer=2, n_head=4, n_embd=256, vocab_size=509, n_positions=64, resid_pdrop=0.0, attn_pdrop=0.0)
 m = GPT2(cfg).to("cuda:0")
-ddp = DistributedDataParallel(m, bucket_mb=0.25)
+Wrap = ShardedDataParallel if os.environ["MODE"] == "fsdp" else DistributedDataParallel
+ddp = Wrap(m, bucket_mb=0.25)
 opt = ddp.configure_optimizers(learning_rate=1e-3)
 g = torch.Generator().manual_seed(5)
 toks = torch.randint(0, 509, (3, 4, 65), generator=g)
@@ -42,12 +43,15 @@ dist.barrier(); dist.destroy_process_group()
 """
 
 
-def test_ddp_two_ranks_matches_single_process(tmp_path):
+@pytest.mark.parametrize("mode", ["ddp", "fsdp"])
+def test_ddp_two_ranks_matches_single_process(tmp_path, mode):
+    """ddp: bucketed all-reduce in the backward; fsdp: reduce-scatter of the grad arena, AdamW on the
+    rank's 1/N slice, all-gather of the updated parameters (parallel.ShardedDataParallel)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     script = tmp_path / "w.py"
     script.write_text(WORKER)
-    env = dict(os.environ, REPO=REPO, GPT2MI_SINGLE_DEVICE="1", GPT2MI_DIST_BACKEND="gloo")
+    env = dict(os.environ, REPO=REPO, MODE=mode, GPT2MI_SINGLE_DEVICE="1", GPT2MI_DIST_BACKEND="gloo")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", "--master-port=29555", str(script)]
     out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
