@@ -196,14 +196,11 @@ __global__ __launch_bounds__(kThreads, 3) void attn_fwd_kernel(const bf16* __res
     const int cur = j & 1;
     const char* Ks = smem + cur * 2 * BKV * 128;
     const char* Vs = Ks + BKV * 128;
-    if (j + 1 < nkv) {
-      tile_load(rk, kbase + (size_t)(j + 1) * BKV * ld, ld);
-      tile_load(rv, vbase + (size_t)(j + 1) * BKV * ld, ld);
-    }
     const int k_lo = j * BKV;
-    if (wave_valid && k_lo <= q_lo + 31) {  // wave-uniform: a key of the tile is visible to a query of the wave
-      const bool diag = k_lo + BKV - 1 > q_lo;
-      f32x4 s[2][4];
+    // wave-uniform: a key of the tile is visible to a query of the wave
+    const bool active = wave_valid && k_lo <= q_lo + 31;
+    f32x4 s[2][4];
+    if (active) {
 #pragma unroll
       for (int fi = 0; fi < 4; ++fi) {
         s[0][fi] = s[1][fi] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -214,6 +211,14 @@ __global__ __launch_bounds__(kThreads, 3) void attn_fwd_kernel(const bf16* __res
           s[1][fi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[1][kk], s[1][fi], 0, 0, 0);
         }
       }
+    }
+    // next K/V tile into registers, issued behind S = K Q^T (its LDS-write point is the end of the tile)
+    if (j + 1 < nkv) {
+      tile_load(rk, kbase + (size_t)(j + 1) * BKV * ld, ld);
+      tile_load(rv, vbase + (size_t)(j + 1) * BKV * ld, ld);
+    }
+    if (active) {
+      const bool diag = k_lo + BKV - 1 > q_lo;
       if (diag) {  // causal mask only on the diagonal tiles (wave-uniform branch)
 #pragma unroll
         for (int qg = 0; qg < 2; ++qg)
@@ -504,8 +509,8 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dkdv_kernel(const bf16* 
   auto gload = [&](int i) {
     tile_load(rq, qbase + (size_t)i * BQT * ld, ld);
     tile_load(rd, dbase + (size_t)i * BQT * C, C);
-    if (threadIdx.x < BQT) {
-      rl = lrow[i * BQT + threadIdx.x] * kLog2e;
+    if (threadIdx.x < BQT) {  // raw values: any use here would wait (in-order vmcnt) for the tiles above too
+      rl = lrow[i * BQT + threadIdx.x];
       rdl = drow[i * BQT + threadIdx.x];
     }
   };
@@ -513,7 +518,7 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dkdv_kernel(const bf16* 
     tile_store(st, rq);
     tile_store(st + kTile, rd);
     if (threadIdx.x < BQT) {
-      reinterpret_cast<float*>(st + 2 * kTile)[threadIdx.x] = rl;
+      reinterpret_cast<float*>(st + 2 * kTile)[threadIdx.x] = rl * kLog2e;
       reinterpret_cast<float*>(st + 2 * kTile + BQT * 4)[threadIdx.x] = rdl;
     }
   };
