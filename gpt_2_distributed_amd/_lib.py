@@ -38,6 +38,7 @@ _SIGS = {
     "gpt2mi_norm_partials_size": [],
     "gpt2mi_cast_f32_bf16": [_p, _p, _c_size, _p],
     "gpt2mi_transpose_bf16": [_p, _p, _c_int, _c_int, _c_int, _c_int, _p],
+    "gpt2mi_transpose_bf16_batched": [_p, _p, _p, _c_int, ctypes.c_int64, _p],
     "gpt2mi_scale_mul": [_p, _p, _p, _p],
     "gpt2mi_memset_zero": [_p, _c_size, _p],
     "gpt2mi_set_gemm_impl": [_c_int],
@@ -212,6 +213,11 @@ def cast_f32_bf16(x, y, n):
 
 def transpose_bf16(src, dst, R, C, ld_src=None, ld_dst=None):
     _call("gpt2mi_transpose_bf16", _ptr(src), _ptr(dst), R, C, ld_src or C, ld_dst or R, _stream())
+
+
+def transpose_bf16_batched(src, dst, desc, n, total_tiles):
+    """desc: device int64 [n, 4] = (element offset, R, C, first tile) per matrix (see include/gpt2mi.h)."""
+    _call("gpt2mi_transpose_bf16_batched", _ptr(src), _ptr(dst), _ptr(desc), n, total_tiles, _stream())
 
 
 def scale_mul(a, b, out):

@@ -28,4 +28,4 @@ int check_launch(const char* what) {
 
 GPT2MI_EXPORT const char* gpt2mi_last_error(void) { return gpt2mi::g_err; }
 
-GPT2MI_EXPORT int gpt2mi_abi_version(void) { return 3; }
+GPT2MI_EXPORT int gpt2mi_abi_version(void) { return 4; }

@@ -9,10 +9,10 @@ namespace {
 
 constexpr int TT = 64;
 
-__global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16* __restrict__ src, bf16* __restrict__ dst,
-                                                            int R, int C, int lds, int ldd) {
+// one 64x64 tile (r0, c0) of src[R][C] (leading dim lds) into dst[C][R] (leading dim ldd)
+__device__ __forceinline__ void transpose_tile(const bf16* __restrict__ src, bf16* __restrict__ dst, int r0, int c0,
+                                               int lds, int ldd) {
   __shared__ bf16 tile[TT][TT + 2];
-  const int r0 = blockIdx.y * TT, c0 = blockIdx.x * TT;
   const int t = threadIdx.x;
   // load: 64 rows x 8 chunks of 8 elements = 512 chunks, 2 per thread
 #pragma unroll
@@ -34,6 +34,24 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16* __restr
   }
 }
 
+__global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16* __restrict__ src, bf16* __restrict__ dst,
+                                                            int R, int C, int lds, int ldd) {
+  transpose_tile(src, dst, blockIdx.y * TT, blockIdx.x * TT, lds, ldd);
+}
+
+// Every weight of the shadow arena in one launch: desc[i] = {element offset, R, C, first tile} (dense
+// [R][C] at src + offset -> [C][R] at dst + offset), blocks walk the flat tile range.
+__global__ __launch_bounds__(256) void transpose_bf16_batched_kernel(const bf16* __restrict__ src,
+                                                                    bf16* __restrict__ dst,
+                                                                    const int64_t* __restrict__ desc, int n) {
+  const int64_t tile = blockIdx.x;
+  int i = 0;
+  while (i + 1 < n && desc[4 * (i + 1) + 3] <= tile) ++i;  // n <= a few hundred: scalar loop
+  const int64_t off = desc[4 * i], R = desc[4 * i + 1], C = desc[4 * i + 2], t = tile - desc[4 * i + 3];
+  const int tc = (int)(C / TT);
+  transpose_tile(src + off, dst + off, (int)(t / tc) * TT, (int)(t % tc) * TT, (int)C, (int)R);
+}
+
 }  // namespace
 
 GPT2MI_EXPORT int gpt2mi_transpose_bf16(const uint16_t* src, uint16_t* dst, int R, int C, int ld_src, int ld_dst,
@@ -45,4 +63,13 @@ GPT2MI_EXPORT int gpt2mi_transpose_bf16(const uint16_t* src, uint16_t* dst, int 
   transpose_bf16_kernel<<<dim3(C / TT, R / TT), 256, 0, (hipStream_t)stream>>>((const bf16*)src, (bf16*)dst, R, C,
                                                                                ld_src, ld_dst);
   return gpt2mi::check_launch("transpose_bf16");
+}
+
+GPT2MI_EXPORT int gpt2mi_transpose_bf16_batched(const uint16_t* src, uint16_t* dst, const int64_t* desc, int n,
+                                                int64_t total_tiles, void* stream) {
+  GPT2MI_REQUIRE(n > 0 && total_tiles > 0 && total_tiles < (1ll << 31), "transpose_bf16_batched: n=%d tiles=%lld", n,
+                 (long long)total_tiles);
+  transpose_bf16_batched_kernel<<<dim3((unsigned)total_tiles), 256, 0, (hipStream_t)stream>>>(
+      (const bf16*)src, (bf16*)dst, desc, n);
+  return gpt2mi::check_launch("transpose_bf16_batched");
 }

@@ -226,12 +226,20 @@ class Engine:
         return self._rows(name) % 64 == 0 and sl.shape[1] % 64 == 0
 
     def _refresh_shadowT(self):
-        for n in self._t_weights:
-            if self.wT_ok(n):
-                sl = self.layout.slots[n]
-                R, Cc = self._rows(n), sl.shape[1]
-                K.transpose_bf16(self.shadow[sl.offset:sl.offset + R * Cc], self.shadowT[sl.offset:sl.offset + R * Cc],
-                                 R, Cc)
+        # every transposable weight in one launch (49 separate 64x64-tile launches cost 0.28 ms per step)
+        if getattr(self, "_tdesc", None) is None:
+            rows, tiles = [], 0
+            for n in self._t_weights:
+                if self.wT_ok(n):
+                    sl = self.layout.slots[n]
+                    R, Cc = self._rows(n), sl.shape[1]
+                    rows.append((sl.offset, R, Cc, tiles))
+                    tiles += (R // 64) * (Cc // 64)
+            self._tdesc = (torch.tensor(rows, dtype=torch.int64, device=self.device) if rows else None, len(rows),
+                           tiles)
+        desc, n, tiles = self._tdesc
+        if n:
+            K.transpose_bf16_batched(self.shadow, self.shadowT, desc, n, tiles)
         self._shadowT_stale = False
 
     def wT16(self, name):  # bf16 W^T view (flat, [in][out_padded])

@@ -134,6 +134,11 @@ void gpt2mi_set_gemm_impl(int impl);
 /* dst[c][r] = src[r][c] for a bf16 [R][C] matrix (R, C multiples of 64): the transposed weight shadow
  * the backward dgrad GEMMs read in the forward (k-contiguous) layout. */
 int gpt2mi_transpose_bf16(const uint16_t* src, uint16_t* dst, int R, int C, int ld_src, int ld_dst, void* stream);
+/* All weights of a shadow arena in one launch: desc (device, int64 [n][4]) = {element offset, R, C, first
+ * tile index} with R, C multiples of 64 and first tiles the prefix sums of (R/64)*(C/64); src + offset is a
+ * dense [R][C] matrix, dst + offset receives its [C][R] transpose. */
+int gpt2mi_transpose_bf16_batched(const uint16_t* src, uint16_t* dst, const int64_t* desc, int n,
+                                  int64_t total_tiles, void* stream);
 int gpt2mi_cast_f32_bf16(const float* x, uint16_t* y, size_t n, void* stream);
 int gpt2mi_scale_mul(const float* a, const float* b, float* out, void* stream);
 int gpt2mi_memset_zero(void* ptr, size_t bytes, void* stream);

@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
     missing = [n for n in declared() if not hasattr(lib, n)]
     assert not missing, missing
     lib.gpt2mi_abi_version.restype = ctypes.c_int
-    assert lib.gpt2mi_abi_version() == 3
+    assert lib.gpt2mi_abi_version() == 4
 
 
 def test_ctypes_binding_covers_the_header():

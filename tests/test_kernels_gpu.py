@@ -479,3 +479,25 @@ def test_gemm_fused_bias_grad(N, epi):
     torch.cuda.synchronize()
     ref = db0.double() + C.cpu().double().sum(0)
     assert rel_err(db.cpu(), ref) < 1e-5
+
+
+def test_transpose_bf16_batched():
+    """Several weights of one arena in one launch (the transposed-shadow refresh) == per-matrix W^T."""
+    shapes = [(128, 64), (192, 320), (64, 64), (256, 128)]
+    offs, o = [], 0
+    for r, c in shapes:
+        offs.append(o)
+        o += r * c + 64  # gaps stay untouched
+    src = bf(torch.randn(o)).to(dev)
+    dst = torch.full((o,), 7.0, dtype=torch.bfloat16, device=dev)
+    rows, tiles = [], 0
+    for (r, c), off in zip(shapes, offs):
+        rows.append((off, r, c, tiles))
+        tiles += (r // 64) * (c // 64)
+    desc = torch.tensor(rows, dtype=torch.int64, device=dev)
+    L().transpose_bf16_batched(src, dst, desc, len(rows), tiles)
+    torch.cuda.synchronize()
+    for (r, c), off in zip(shapes, offs):
+        w = src[off:off + r * c].view(r, c)
+        assert torch.equal(dst[off:off + r * c].view(c, r), w.t()), (r, c)
+        assert torch.all(dst[off + r * c:off + r * c + 64] == 7.0)
