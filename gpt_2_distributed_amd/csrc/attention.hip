@@ -117,6 +117,29 @@ __device__ __forceinline__ void tile_load(u32x4* r, const bf16* src, size_t ld) 
     r[i] = *reinterpret_cast<const u32x4*>(src + (size_t)(id >> 3) * ld + 8 * (id & 7));
   }
 }
+typedef __attribute__((address_space(3))) void lds_void;
+// 64 rows x 128 B tile by LDS-DMA (global_load_lds_dwordx4, no register staging): instruction `ins` (of
+// wave w: ins = 2w, 2w+1) writes LDS bytes [1024*ins, +1024) = rows 8*ins .. 8*ins+7; the t_off swizzle is applied on
+// the source address (slot s of row r holds chunk s ^ (r & 6)).
+// A lane's source offset is the same for every instruction: one VGPR per lane; the tile / row-group
+// position is a wave-uniform byte offset (SGPR soffset) into a raw buffer over the batch row's qkv.
+__device__ __forceinline__ uint32_t tile_dma_off(size_t ld, int lane) {
+  const int r = lane >> 3;
+  return (uint32_t)((r * ld + 8 * ((lane & 7) ^ (r & 6))) * sizeof(bf16));
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t qkv_rsrc(const bf16* base) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
+}
+// rows [row0, row0 + 64) x cols [col0, col0 + 64) of the buffer (row stride ld elements)
+__device__ __forceinline__ void tile_dma(char* lds, __amdgpu_buffer_rsrc_t rs, int row0, int col0, int ld,
+                                         uint32_t loff, int w) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int ins = 2 * w + i;
+    const int soff = ((row0 + 8 * ins) * ld + col0) * (int)sizeof(bf16);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(lds + ins * 1024), 16, loff, soff, 0, 0);
+  }
+}
 __device__ __forceinline__ void tile_store(char* base, const u32x4* r) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -147,7 +170,7 @@ __device__ __forceinline__ void attn_block(int& bh, int& blk) {
 
 // ---------------------------------------------------------------------------------------------
 template <bool DROP>
-__global__ __launch_bounds__(kThreads, 3) void attn_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
+__global__ __launch_bounds__(kThreads, DROP ? 4 : 3) void attn_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
                                                                float* __restrict__ lse, int T, int H, float scale,
                                                                uint64_t seed, uint32_t thr, float inv_keep) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * BKV * 128];  // 2 stages x (K, V)
@@ -182,15 +205,13 @@ __global__ __launch_bounds__(kThreads, 3) void attn_fwd_kernel(const bf16* __res
   const bf16 one = (bf16)1.f;
   const bf16x8 ones = {one, one, one, one, one, one, one, one};
 
-  u32x4 rk[2], rv[2];
-  const bf16* kbase = base + C + h * D;
-  const bf16* vbase = base + 2 * C + h * D;
   const int nkv = min((qb + 1) * BQ, T) / BKV;
-  tile_load(rk, kbase, ld);
-  tile_load(rv, vbase, ld);
-  tile_store(smem, rk);
-  tile_store(smem + BKV * 128, rv);
-  __syncthreads();
+  const uint32_t loff = tile_dma_off(ld, lane);
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const __amdgpu_buffer_rsrc_t rs = qkv_rsrc(base);
+  tile_dma(smem, rs, 0, C + h * D, (int)ld, loff, wu);
+  tile_dma(smem + BKV * 128, rs, 0, 2 * C + h * D, (int)ld, loff, wu);
+  __syncthreads();  // waits for this wave's DMAs (vmcnt(0)), then for every wave's
 
   for (int j = 0; j < nkv; ++j) {
     const int cur = j & 1;
@@ -212,10 +233,12 @@ __global__ __launch_bounds__(kThreads, 3) void attn_fwd_kernel(const bf16* __res
         }
       }
     }
-    // next K/V tile into registers, issued behind S = K Q^T (its LDS-write point is the end of the tile)
+    // next K/V tile straight into the other LDS stage (read last in tile j-1, released by its barrier),
+    // issued behind S = K Q^T; it lands while this tile's softmax and P.V run
     if (j + 1 < nkv) {
-      tile_load(rk, kbase + (size_t)(j + 1) * BKV * ld, ld);
-      tile_load(rv, vbase + (size_t)(j + 1) * BKV * ld, ld);
+      char* nxt = smem + (cur ^ 1) * 2 * BKV * 128;
+      tile_dma(nxt, rs, (j + 1) * BKV, C + h * D, (int)ld, loff, wu);
+      tile_dma(nxt + BKV * 128, rs, (j + 1) * BKV, 2 * C + h * D, (int)ld, loff, wu);
     }
     if (active) {
       const bool diag = k_lo + BKV - 1 > q_lo;
@@ -283,11 +306,6 @@ __global__ __launch_bounds__(kThreads, 3) void attn_fwd_kernel(const bf16* __res
           o[1][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vt, p1, o[1][fd], 0, 0, 0);
         }
       }
-    }
-    if (j + 1 < nkv) {
-      char* nxt = smem + (cur ^ 1) * 2 * BKV * 128;
-      tile_store(nxt, rk);
-      tile_store(nxt + BKV * 128, rv);
     }
     __syncthreads();
   }
@@ -361,22 +379,21 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const bf16* __
 #pragma unroll
     for (int f = 0; f < 4; ++f) dq[qg][f] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  u32x4 rk[2], rv[2];
-  const bf16* kbase = base + C + h * D;
-  const bf16* vbase = base + 2 * C + h * D;
   const int nkv = min((qb + 1) * BQ, T) / BKV;
-  tile_load(rk, kbase, ld);
-  tile_load(rv, vbase, ld);
-  tile_store(smem, rk);
-  tile_store(smem + BKV * 128, rv);
+  const uint32_t loff = tile_dma_off(ld, lane);
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const __amdgpu_buffer_rsrc_t rs = qkv_rsrc(base);
+  tile_dma(smem, rs, 0, C + h * D, (int)ld, loff, wu);
+  tile_dma(smem + BKV * 128, rs, 0, 2 * C + h * D, (int)ld, loff, wu);
   __syncthreads();
   for (int j = 0; j < nkv; ++j) {
     const int cur = j & 1;
     const char* Ks = smem + cur * 2 * BKV * 128;
     const char* Vs = Ks + BKV * 128;
-    if (j + 1 < nkv) {
-      tile_load(rk, kbase + (size_t)(j + 1) * BKV * ld, ld);
-      tile_load(rv, vbase + (size_t)(j + 1) * BKV * ld, ld);
+    if (j + 1 < nkv) {  // next K/V tile by LDS-DMA into the stage released by tile j-1's barrier
+      char* nxt = smem + (cur ^ 1) * 2 * BKV * 128;
+      tile_dma(nxt, rs, (j + 1) * BKV, C + h * D, (int)ld, loff, wu);
+      tile_dma(nxt + BKV * 128, rs, (j + 1) * BKV, 2 * C + h * D, (int)ld, loff, wu);
     }
     const int k_lo = j * BKV;
     if (wave_valid && k_lo <= q_lo + 31) {
@@ -432,11 +449,6 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const bf16* __
           dq[1][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kt, s1, dq[1][fd], 0, 0, 0);
         }
       }
-    }
-    if (j + 1 < nkv) {
-      char* nxt = smem + (cur ^ 1) * 2 * BKV * 128;
-      tile_store(nxt, rk);
-      tile_store(nxt + BKV * 128, rv);
     }
     __syncthreads();
   }
@@ -499,31 +511,30 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dkdv_kernel(const bf16* 
   for (int kg = 0; kg < 2; ++kg)
 #pragma unroll
     for (int f = 0; f < 4; ++f) dk[kg][f] = dv[kg][f] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const bf16* qbase = base + h * D;
-  const bf16* dbase = dout + (size_t)b * T * C + h * D;
   const float* lrow = lse + (size_t)bh * T;
   const float* drow = delta + (size_t)bh * T;
 
-  u32x4 rq[2], rd[2];
   float rl = 0.f, rdl = 0.f;
-  auto gload = [&](int i) {
-    tile_load(rq, qbase + (size_t)i * BQT * ld, ld);
-    tile_load(rd, dbase + (size_t)i * BQT * C, C);
+  const uint32_t qoff = tile_dma_off(ld, lane), doff = tile_dma_off(C, lane);
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const __amdgpu_buffer_rsrc_t rsq = qkv_rsrc(base), rsd = qkv_rsrc(dout + (size_t)b * T * C);
+  // Q / dO tiles by LDS-DMA straight into stage `st`; lse / delta by registers (scaled at their LDS write)
+  auto gload = [&](int i, char* st) {
+    tile_dma(st, rsq, i * BQT, h * D, (int)ld, qoff, wu);
+    tile_dma(st + kTile, rsd, i * BQT, h * D, C, doff, wu);
     if (threadIdx.x < BQT) {  // raw values: any use here would wait (in-order vmcnt) for the tiles above too
       rl = lrow[i * BQT + threadIdx.x];
       rdl = drow[i * BQT + threadIdx.x];
     }
   };
   auto sstore = [&](char* st) {
-    tile_store(st, rq);
-    tile_store(st + kTile, rd);
     if (threadIdx.x < BQT) {
       reinterpret_cast<float*>(st + 2 * kTile)[threadIdx.x] = rl * kLog2e;
       reinterpret_cast<float*>(st + 2 * kTile + BQT * 4)[threadIdx.x] = rdl;
     }
   };
   const int i0 = kb * BKB / BQT;
-  gload(i0);
+  gload(i0, smem);
   sstore(smem);
   __syncthreads();
   for (int i = i0; i < nqt; ++i) {
@@ -532,7 +543,7 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dkdv_kernel(const bf16* 
     const char* Ds = Qs + kTile;
     const float* Ls = reinterpret_cast<const float*>(Qs + 2 * kTile);
     const float* Dl = Ls + BQT;
-    if (i + 1 < nqt) gload(i + 1);
+    if (i + 1 < nqt) gload(i + 1, smem + (cur ^ 1) * kStage);
     const int q0 = i * BQT;
     if (wave_valid && q0 + BQT - 1 >= k_lo) {  // wave-uniform: a query of the tile sees a key of the wave
       const bool diag = q0 < k_lo + 31;
