@@ -353,12 +353,14 @@ def test_attention_dropout_stats_and_grad_consistency():
     assert abs(lhs - rhs) < 2e-3 * scale, (lhs, rhs, scale)
 
 
-@pytest.mark.parametrize("M,V,ld", [(64, 509, 512), (128, 50257, 50304)])
+@pytest.mark.parametrize("M,V,ld", [(64, 509, 512), (128, 50257, 50304), (600, 50257, 50432)])
 def test_xent(M, V, ld):
-    g = torch.Generator().manual_seed(V)
+    """M = 600 > the row-pipelined kernel's 256 blocks: blocks walk several rows."""
+    g = torch.Generator().manual_seed(V + M)
     logits = bf(torch.randn(M, ld, generator=g) * 3)
     labels = torch.randint(0, V, (M,), generator=g)
     labels[3] = -100
+    labels[5], labels[7], labels[M - 1] = V - 1, 0, -100  # label in the tail chunk / first column
     lg = logits[:, :V].float().requires_grad_(True)
     ref = torch.nn.functional.cross_entropy(lg, labels, ignore_index=-100)
     ref.backward()
@@ -371,7 +373,8 @@ def test_xent(M, V, ld):
     L().xent_fwd(ld_, ld, labels.to(dev), rows, lse, dl, ld, M, V, loss, inv)
     torch.cuda.synchronize()
     assert abs(loss.item() - ref.item()) < 1e-5 * max(1.0, ref.item())
-    assert abs(inv.item() - 1.0 / (M - 1)) < 1e-9
+    assert abs(inv.item() - 1.0 / (M - 2)) < 1e-9
+    assert rows[3].item() == 0.0 and rows[M - 1].item() == 0.0
     grad = dl.cpu().float()[:, :V] * inv.item()
     assert rel_err(grad, lg.grad) < 4e-3
     assert torch.all(dl[:, V:] == 0)

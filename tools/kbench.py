@@ -99,12 +99,48 @@ def gemm(M=65536):
     print(f"[torch/hipBLASLt reference] fc1 fwd: {ms:.3f} ms {2.0*M*4*C*C/ms/1e9:.0f} TF")
 
 
+def mem(M=65536, C=768, Vp=50432, V=50257):
+    """Bandwidth-bound kernels at their step shapes; GB/s from algorithmic bytes."""
+    g = torch.Generator(device=dev).manual_seed(0)
+    logits = (torch.randn(M, Vp, device=dev, generator=g) * 2).to(torch.bfloat16)
+    labels = torch.randint(0, V, (M,), device=dev, generator=g)
+    dl = torch.empty_like(logits)
+    lr, lse = torch.empty(M, device=dev), torch.empty(M, device=dev)
+    loss, ic = torch.empty(1, device=dev), torch.empty(1, device=dev)
+    ms = timeit(lambda: K.xent_fwd(logits, Vp, labels, lr, lse, dl, Vp, M, V, loss, ic), reps=10)
+    print(f"xent             {ms:7.3f} ms {4.0 * M * Vp / ms / 1e6:6.0f} GB/s")
+    del logits, dl
+    x = torch.randn(M, C, device=dev, generator=g)
+    w, b = torch.ones(C, device=dev), torch.zeros(C, device=dev)
+    y = torch.empty(M, C, device=dev, dtype=torch.bfloat16)
+    mean, rstd = torch.empty(M, device=dev), torch.empty(M, device=dev)
+    ms = timeit(lambda: K.layernorm_fwd(x, w, b, y, None, mean, rstd, M, C, 1e-5), reps=20)
+    print(f"ln fwd           {ms:7.3f} ms {(6.0 * M * C + 8 * M) / ms / 1e6:6.0f} GB/s")
+    dy = torch.randn(M, C, device=dev, generator=g).to(torch.bfloat16)
+    dres = torch.zeros(M, C, device=dev)
+    dw, db, dbo = torch.zeros(C, device=dev), torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+    ob = torch.empty(M, C, device=dev, dtype=torch.bfloat16)
+    ms = timeit(lambda: K.layernorm_bwd(x, w, mean, rstd, dy, dres, dw, db, ob, dbo, M, C, 0.1, 7), reps=20)
+    print(f"ln bwd           {ms:7.3f} ms {16.0 * M * C / ms / 1e6:6.0f} GB/s (16 B/element)")
+    del x, dy, dres, ob, y
+    n = 124475904
+    pp, gg, m1, v1 = (torch.randn(n, device=dev, generator=g) for _ in range(4))
+    v1.abs_()
+    pb = torch.empty(n, device=dev, dtype=torch.bfloat16)
+    part = torch.empty(K.norm_partials_size(), device=dev)
+    gn = torch.empty(1, device=dev)
+    ms = timeit(lambda: K.adamw(pp, gg, m1, v1, pb, n, 1e-4, 0.1, 0.9, 0.95, 1e-8, 1, 1.0, part, gn), reps=10)
+    print(f"adamw            {ms:7.3f} ms {30.0 * n / ms / 1e6:6.0f} GB/s (30 B/param)")
+
+
 if __name__ == "__main__":
     what = sys.argv[1:] or ["attn", "gemm"]
     K.load()
     if "attn" in what:
         attn(p=0.0)
         attn(p=0.1)
+    if "mem" in what:
+        mem()
     if "gemm" in what:
         impls = [int(a[5:]) for a in sys.argv[1:] if a.startswith("impl=")] or [0, 2]
         for impl in impls:
