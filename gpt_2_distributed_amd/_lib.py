@@ -16,6 +16,10 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # GPT2MI_LIB: an alternative build of the same library (A/B kernel experiments, tools/kbench.py)
 LIB_PATH = os.environ.get("GPT2MI_LIB") or os.path.join(_HERE, "libgpt2mi.so")
 
+# the ABI these bindings are written against (include/gpt2mi.h GPT2MI_ABI_VERSION): a stale or foreign
+# library is refused at load instead of being called with the wrong argument lists
+ABI_VERSION = 4
+
 _c_int, _c_float, _c_size, _c_u64, _p = ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_void_p
 
 # name -> argtypes (all return int status unless listed in _RESTYPES)
@@ -77,6 +81,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = _RESTYPES.get(name, ctypes.c_int)
+    if lib.gpt2mi_abi_version() != ABI_VERSION:
+        raise KernelError(f"{path} has C ABI v{lib.gpt2mi_abi_version()}, the bindings expect v{ABI_VERSION}: rebuild it")
     _lib = lib
     return lib
 

@@ -5,6 +5,7 @@
 #include <string.h>
 
 #include "common.h"
+#include "gpt2mi.h"
 
 namespace gpt2mi {
 static thread_local char g_err[512] = "";
@@ -28,4 +29,4 @@ int check_launch(const char* what) {
 
 GPT2MI_EXPORT const char* gpt2mi_last_error(void) { return gpt2mi::g_err; }
 
-GPT2MI_EXPORT int gpt2mi_abi_version(void) { return 4; }
+GPT2MI_EXPORT int gpt2mi_abi_version(void) { return GPT2MI_ABI_VERSION; }

@@ -26,8 +26,10 @@
 extern "C" {
 #endif
 
+#define GPT2MI_ABI_VERSION 4
+
 const char* gpt2mi_last_error(void);
-int gpt2mi_abi_version(void);
+int gpt2mi_abi_version(void); /* returns GPT2MI_ABI_VERSION of the built library */
 
 /* K1: x[b,t,:] = drop(wte[idx[b,t],:] + wpe[t,:])  — model.py:295-304 (embedding, add, dropout). */
 int gpt2mi_embed_fwd(const int64_t* idx, const float* wte, const float* wpe, float* x, int B, int T, int C,

@@ -31,7 +31,9 @@ def test_library_exports_every_declared_symbol():
     missing = [n for n in declared() if not hasattr(lib, n)]
     assert not missing, missing
     lib.gpt2mi_abi_version.restype = ctypes.c_int
-    assert lib.gpt2mi_abi_version() == 4
+    from gpt_2_distributed_amd import _lib
+    hdr = re.search(r"#define GPT2MI_ABI_VERSION (\d+)", open(HEADER).read())
+    assert lib.gpt2mi_abi_version() == _lib.ABI_VERSION == int(hdr.group(1))
 
 
 def test_ctypes_binding_covers_the_header():
