@@ -1,7 +1,7 @@
 """Launch ONE of bench.py's probed kernels a few times on step-shaped inputs (GPT-2 124M, B=64, T=1024,
 dropout 0.1), for the rocprofv3 --pmc traffic passes (tools/pmc_traffic.sh -> profiles/traffic.json).
 
-    python tools/kernel_one.py <lm_head_fwd|lm_head_dgrad|lm_head_wgrad|fc1_fwd|attn_fwd> [reps]
+    python tools/kernel_one.py <lm_head_fwd|lm_head_dgrad|lm_head_wgrad|fc1_fwd|attn_fwd|attn_bwd> [reps]
 """
 import os
 import sys
@@ -42,6 +42,13 @@ def make(name):
         lse = torch.empty(B * H, T, device=dev)
         p = float(os.environ.get("ATTN_P", "0.1"))
         return lambda: K.attn_fwd(qkv, out, lse, B, T, H, C // H, p, 5)
+    if name == "attn_bwd":  # dQ (+ delta) then dK/dV
+        qkv, out, dout = r(M, 3 * C), r(M, C), r(M, C)
+        lse = torch.randn(B * H, T, device=dev).abs() + 5.0
+        delta = torch.empty(B * H, T, device=dev)
+        dqkv = torch.empty(M, 3 * C, dtype=torch.bfloat16, device=dev)
+        p = float(os.environ.get("ATTN_P", "0.1"))
+        return lambda: K.attn_bwd(qkv, out, dout, lse, delta, dqkv, B, T, H, C // H, p, 5)
     raise SystemExit(f"unknown kernel {name}")
 
 
