@@ -1,7 +1,47 @@
+"""Reference point, not product code: torch (hipBLASLt) on the step's plain GEMM shapes, HIP-event timed,
+next to the same shapes through libgpt2mi. Run under rocprofv3 --kernel-trace to see hipBLASLt's kernel names.
+
+    python tools/hipblaslt_probe.py
+"""
+import os
+import sys
+
 import torch
-A = torch.randn(65536, 768, device="cuda").to(torch.bfloat16)
-W = torch.randn(50432, 768, device="cuda").to(torch.bfloat16)
-W2 = torch.randn(3072, 768, device="cuda").to(torch.bfloat16)
-for _ in range(3):
-    y = A @ W.t(); z = A @ W2.t()
-torch.cuda.synchronize()
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from gpt_2_distributed_amd import _lib as K  # noqa: E402
+
+dev = "cuda"
+M, C, Vp = 65536, 768, 50432
+
+
+def timeit(fn, reps=10):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+def r(*s):
+    return (torch.randn(*s, device=dev) * 0.5).to(torch.bfloat16)
+
+
+K.load()
+# (name, M, N, K): out[M,N] = A[M,K] . W[N,K]^T   (forward layout; dgrads run against the transposed shadow)
+shapes = [("lm_head fwd", M, Vp, C), ("qkv fwd", M, 3 * C, C), ("fc1 fwd (plain)", M, 4 * C, C),
+          ("proj fwd (plain)", M, C, C), ("lm dgrad", M, C, Vp), ("qkv dgrad", M, C, 3 * C),
+          ("fc1 dgrad", M, C, 4 * C)]
+for name, m, n, k in shapes:
+    a, w = r(m, k), r(n, k)
+    out = torch.empty(m, n, dtype=torch.bfloat16, device=dev)
+    t_blt = timeit(lambda: torch.mm(a, w.t(), out=out))
+    t_own = timeit(lambda: K.gemm(K.FWD, K.EPI_BF16, m, n, k, a, k, w, k, out, n))
+    f = 2.0 * m * n * k
+    print(f"{name:18s} hipBLASLt {t_blt:7.3f} ms {f / t_blt / 1e9:6.0f} TF | libgpt2mi {t_own:7.3f} ms {f / t_own / 1e9:6.0f} TF")
+    del a, w, out
