@@ -19,6 +19,7 @@ Also reported:
                host's cores on a bounded sample (rank 0, N = 1 only)
 """
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -66,6 +67,10 @@ def main():
     ap.add_argument("--dropout", type=float, default=0.1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
+    # BASELINE configs 4-5 (350M / 1.5B under FSDP, 1.5B with gradient accumulation); a "step" is then one
+    # optimizer step over grad_accum micro-batches of --batch sequences per rank
+    ap.add_argument("--parallel", choices=["ddp", "fsdp"], default="ddp", help="multi-rank wrapper (N > 1)")
+    ap.add_argument("--grad_accum", type=int, default=1)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -83,8 +88,9 @@ def main():
     model = GPT2(cfg).to(dev)
     model.train()
     if world > 1:
-        from gpt_2_distributed_amd.parallel import DistributedDataParallel
-        ddp = DistributedDataParallel(model, bucket_mb=args.bucket_mb)
+        from gpt_2_distributed_amd.parallel import DistributedDataParallel, ShardedDataParallel
+        wrap = ShardedDataParallel if args.parallel == "fsdp" else DistributedDataParallel
+        ddp = wrap(model, bucket_mb=args.bucket_mb)
         opt = ddp.configure_optimizers(learning_rate=1e-4)
         fwd = ddp
     else:
@@ -99,11 +105,17 @@ def main():
         t = torch.randint(0, cfg.vocab_size, (B, T + 1), generator=g)
         batches.append((t[:, :-1].contiguous().to(dev), t[:, 1:].contiguous().to(dev)))
 
+    GA = args.grad_accum
+
     def step(i):
-        x, y = batches[i % len(batches)]
-        with torch.autocast("cuda", dtype=torch.bfloat16):  # the reference trainer's step (:404)
-            _, loss = fwd(x, labels=y)
-        loss.backward()
+        for a in range(GA):  # the reference loop (:400-425): no_sync on all but the last micro-step
+            x, y = batches[(i * GA + a) % len(batches)]
+            ctx = fwd.no_sync() if (a + 1 < GA and hasattr(fwd, "no_sync")) else contextlib.nullcontext()
+            with ctx:
+                with torch.autocast("cuda", dtype=torch.bfloat16):  # the reference trainer's step (:404)
+                    _, loss = fwd(x, labels=y)
+                    loss = loss / GA
+                loss.backward()
         opt.step()
         opt.zero_grad()
         return loss
@@ -162,7 +174,7 @@ def main():
                     "unit": "TFLOP/s", "frac": k["frac_of_peak"], "traffic": traffic,
                     "algorithmic_flop_per_launch": kflops[dom]}
 
-    tokens = world * B * T * args.steps
+    tokens = world * B * T * GA * args.steps
     tok_s = tokens / dt
     fpt = flops_per_token(cfg, T)
     out = {
@@ -179,12 +191,12 @@ def main():
         "dtype": "bf16",
         "data": "synthetic (uniform random tokens, resident in HBM)",
         "config": {"workload": f"GPT-2 {args.model} training step: fwd+loss+bwd+grad-allreduce+AdamW, "
-                               f"dropout {args.dropout}",
-                   "model": f"GPT-2 {args.model}", "global_batch": B * world, "seq_len": T,
-                   "parallelism": f"dp{world}"},
+                               f"dropout {args.dropout}" + (f", {GA} accumulated micro-batches" if GA > 1 else ""),
+                   "model": f"GPT-2 {args.model}", "global_batch": B * world * GA, "seq_len": T,
+                   "parallelism": f"{'fsdp' if args.parallel == 'fsdp' and world > 1 else 'dp'}{world}"},
         "mfu": round(tok_s * fpt / (world * PEAK_BF16_TFLOPS * 1e12), 4),
         "flop_per_token": fpt,
-        "final_loss": round(final_loss, 4),
+        "final_loss": round(final_loss * GA, 4),
         "roofline": roofline,
         "kernels": kernels,
         "cpu_baseline": None,
