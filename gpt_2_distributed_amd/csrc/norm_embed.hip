@@ -144,27 +144,38 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
 #pragma unroll
   for (int i = 0; i < NV * VEC; ++i) adw[i] = adb[i] = abo[i] = 0.f;
 
+  float wv[NV * VEC];  // gamma: the lane's columns, loop-invariant
+#pragma unroll
+  for (int i = 0; i < NV; ++i) load_vec<VEC>(w + VEC * (lane + 64 * i), wv + VEC * i);
   for (int row = row0; row < M; row += stride) {
     const float mu = mean[row], rs = rstd[row];
     const float* xr = x + (size_t)row * C;
     const TG* gr = dy + (size_t)row * C;
-    float xh[NV * VEC], g[NV * VEC];
+    float* dr = dres + (size_t)row * C;
+    float xh[NV * VEC], g[NV * VEC], rd[NV * VEC];
     float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {  // every load of the row first (the residual grad too): one round trip
+      const int e = VEC * (lane + 64 * i);
+      load_vec<VEC>(xr + e, xh + VEC * i);
+      load_t<VEC, TG>(gr + e, g + VEC * i);
+      if (dres_init) {
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) rd[VEC * i + j] = 0.f;
+      } else {
+        load_vec<VEC>(dr + e, rd + VEC * i);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < NV; ++i)
       {
-        const int e = VEC * (lane + 64 * i);
-        float wv[VEC];
-        load_vec<VEC>(xr + e, xh + VEC * i);
-        load_t<VEC, TG>(gr + e, g + VEC * i);
-        load_vec<VEC>(w + e, wv);
 #pragma unroll
         for (int j = 0; j < VEC; ++j) {
           const int k = VEC * i + j;
           xh[k] = (xh[k] - mu) * rs;
           adw[k] += g[k] * xh[k];
           adb[k] += g[k];
-          const float gw = g[k] * wv[j];
+          const float gw = g[k] * wv[k];
           g[k] = gw;
           s1 += gw;
           s2 += gw * xh[k];
@@ -172,22 +183,15 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
       }
     const float m1 = wave_sum(s1) / (float)C;
     const float m2 = wave_sum(s2) / (float)C;
-    float* dr = dres + (size_t)row * C;
 #pragma unroll
     for (int i = 0; i < NV; ++i)
       {
         const int e = VEC * (lane + 64 * i);
         float r[VEC];
-        if (dres_init) {
-#pragma unroll
-          for (int j = 0; j < VEC; ++j) r[j] = 0.f;
-        } else {
-          load_vec<VEC>(dr + e, r);
-        }
 #pragma unroll
         for (int j = 0; j < VEC; ++j) {
           const int k = VEC * i + j;
-          r[j] += rs * (g[k] - m1 - xh[k] * m2);
+          r[j] = rd[k] + rs * (g[k] - m1 - xh[k] * m2);
         }
         store_vec<VEC>(dr + e, r);
         if (out_bf) {
