@@ -109,20 +109,12 @@ __device__ __forceinline__ bf16x8 pack_perm(const f32x4* acc, int kk) {
   return r;
 }
 
-// 64 rows x 128 B tile from a strided global matrix: 2 x 16-B chunks per thread.
-__device__ __forceinline__ void tile_load(u32x4* r, const bf16* src, size_t ld) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int id = threadIdx.x + kThreads * i;
-    r[i] = *reinterpret_cast<const u32x4*>(src + (size_t)(id >> 3) * ld + 8 * (id & 7));
-  }
-}
 typedef __attribute__((address_space(3))) void lds_void;
-// 64 rows x 128 B tile by LDS-DMA (global_load_lds_dwordx4, no register staging): instruction `ins` (of
-// wave w: ins = 2w, 2w+1) writes LDS bytes [1024*ins, +1024) = rows 8*ins .. 8*ins+7; the t_off swizzle is applied on
-// the source address (slot s of row r holds chunk s ^ (r & 6)).
-// A lane's source offset is the same for every instruction: one VGPR per lane; the tile / row-group
-// position is a wave-uniform byte offset (SGPR soffset) into a raw buffer over the batch row's qkv.
+// 64 rows x 128 B tiles arrive by LDS-DMA (buffer_load_dwordx4 ... lds, no register staging): instruction
+// `ins` (of wave w: ins = 2w, 2w+1) writes LDS bytes [1024*ins, +1024) = rows 8*ins .. 8*ins+7, and the
+// t_off swizzle is applied on the source side (slot s of row r holds chunk s ^ (r & 6)). A lane's source
+// offset is the same for every instruction (one VGPR); the tile / row-group position is a wave-uniform
+// byte offset (SGPR soffset) into a raw buffer over one batch row's qkv (or dO).
 __device__ __forceinline__ uint32_t tile_dma_off(size_t ld, int lane) {
   const int r = lane >> 3;
   return (uint32_t)((r * ld + 8 * ((lane & 7) ^ (r & 6))) * sizeof(bf16));
@@ -138,13 +130,6 @@ __device__ __forceinline__ void tile_dma(char* lds, __amdgpu_buffer_rsrc_t rs, i
     const int ins = 2 * w + i;
     const int soff = ((row0 + 8 * ins) * ld + col0) * (int)sizeof(bf16);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(lds + ins * 1024), 16, loff, soff, 0, 0);
-  }
-}
-__device__ __forceinline__ void tile_store(char* base, const u32x4* r) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int id = threadIdx.x + kThreads * i;
-    *reinterpret_cast<u32x4*>(base + t_off(id >> 3, id & 7)) = r[i];
   }
 }
 
