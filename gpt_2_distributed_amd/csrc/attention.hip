@@ -637,6 +637,8 @@ GPT2MI_EXPORT int gpt2mi_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse
                                   float p_drop, uint64_t seed, void* stream) {
   GPT2MI_REQUIRE(head_dim == D, "attn_fwd: head_dim=%d (only 64 is built)", head_dim);
   GPT2MI_REQUIRE(T % 64 == 0 && T > 0, "attn_fwd: T=%d must be a multiple of 64", T);
+  GPT2MI_REQUIRE((size_t)T * 3 * H * D * sizeof(bf16) < (1ull << 31),
+                 "attn_fwd: T*3C too large for the 32-bit buffer offsets of one batch row (T=%d)", T);
   const float scale = 1.f / sqrtf((float)head_dim);
   dim3 grid((T + BQ - 1) / BQ, B * H);
   const uint32_t thr = drop_threshold(p_drop);
@@ -655,6 +657,8 @@ GPT2MI_EXPORT int gpt2mi_attn_bwd(const uint16_t* qkv, const uint16_t* out, cons
                                   int head_dim, float p_drop, uint64_t seed, void* stream) {
   GPT2MI_REQUIRE(head_dim == D, "attn_bwd: head_dim=%d (only 64 is built)", head_dim);
   GPT2MI_REQUIRE(T % 64 == 0 && T > 0, "attn_bwd: T=%d must be a multiple of 64", T);
+  GPT2MI_REQUIRE((size_t)T * 3 * H * D * sizeof(bf16) < (1ull << 31),
+                 "attn_bwd: T*3C too large for the 32-bit buffer offsets of one batch row (T=%d)", T);
   hipStream_t s = (hipStream_t)stream;
   const float scale = 1.f / sqrtf((float)head_dim);
   const uint32_t thr = drop_threshold(p_drop);
