@@ -121,13 +121,24 @@ __global__ __launch_bounds__(kThreads, 1) void gemm256_kernel(GemmParams P) {
         if constexpr (!B_T) bf[j] = frag_kc(Bs, wn * 64 + 16 * j + (lane & 15), 4 * kk + (lane >> 4));
         else bf[j] = frag_mc(Bs, 32 * kk, wn * 64 + 16 * j, lane);
       }
+      if constexpr (A_T && B_T) {
+        bf16x8 af[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        bf16x8 af;
-        if constexpr (!A_T) af = frag_kc(As, wm * 128 + 16 * i + (lane & 15), 4 * kk + (lane >> 4));
-        else af = frag_mc(As, 32 * kk, wm * 128 + 16 * i, lane);
+        for (int i = 0; i < 8; ++i) af[i] = frag_mc(As, 32 * kk, wm * 128 + 16 * i, lane);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af, acc[i][j], 0, 0, 0);
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[i][j], 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          bf16x8 af;
+          if constexpr (!A_T) af = frag_kc(As, wm * 128 + 16 * i + (lane & 15), 4 * kk + (lane >> 4));
+          else af = frag_mc(As, 32 * kk, wm * 128 + 16 * i, lane);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af, acc[i][j], 0, 0, 0);
+        }
       }
     }
     asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
