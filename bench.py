@@ -37,8 +37,9 @@ def flops_per_token(cfg, T):
     return 6 * (L * 12 * C * C + V * C) + 12 * L * T * C
 
 
-def cpu_baseline(batch=2, seq_len=1024, steps=2):
-    """The oracle's fp32 CPU step (same model/seq_len; bounded sample: B=2, timed after 1 warm-up step)."""
+def cpu_baseline(batch=4, seq_len=1024, steps=3):
+    """The oracle's fp32 CPU step on BASELINE cfg 1's shape (124M, B=4, T=1024; bounded sample: 3 timed
+    steps after 1 warm-up step, about 15-30 s of CPU work)."""
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from oracle import model_ref, train_ref
     cfg = model_ref.Cfg(resid_pdrop=0.0, attn_pdrop=0.0, n_positions=seq_len)
@@ -190,8 +191,11 @@ def main():
         "vs_baseline": None,
         "dtype": "bf16",
         "data": "synthetic (uniform random tokens, resident in HBM)",
-        "config": {"workload": f"GPT-2 {args.model} training step: fwd+loss+bwd+grad-allreduce+AdamW, "
-                               f"dropout {args.dropout}" + (f", {GA} accumulated micro-batches" if GA > 1 else ""),
+        "config": {"workload": f"GPT-2 {args.model} training step: fwd+loss+bwd+AdamW"
+                               + ({"ddp": " + bucketed grad all-reduce in the backward",
+                                   "fsdp": " + per-block FSDP all-gather / reduce-scatter"}[args.parallel]
+                                  if world > 1 else "")
+                               + f", dropout {args.dropout}" + (f", {GA} accumulated micro-batches" if GA > 1 else ""),
                    "model": f"GPT-2 {args.model}", "global_batch": B * world * GA, "seq_len": T,
                    "parallelism": f"{'fsdp' if args.parallel == 'fsdp' and world > 1 else 'dp'}{world}"},
         "mfu": round(tok_s * fpt / (world * PEAK_BF16_TFLOPS * 1e12), 4),

@@ -1,0 +1,12 @@
+"""MI355X-native GPT-2 training step: a drop-in for dpickem/gpt_2_distributed's model.py /
+dataloader.py / train_gpt2_distributed.py surfaces, running on hand-written gfx950 HIP kernels
+(libgpt2mi.so, C ABI in include/gpt2mi.h)."""
+from .model import (GPT, GPT2, GPT2Backbone, GPT2Block, GPT2Config, MLP, MODEL_SIZES,  # noqa: F401
+                    CausalMultiHeadSelfAttention, NewGELU)
+from .parallel import DistributedDataParallel, ShardedDataParallel, init_distributed  # noqa: F401
+
+DEFAULT_CONFIG = GPT2Config()  # train_gpt2_distributed.py:42-44 (124M; --seq_len replaces n_positions)
+
+__all__ = ["GPT", "GPT2", "GPT2Backbone", "GPT2Block", "GPT2Config", "MLP", "CausalMultiHeadSelfAttention",
+           "NewGELU", "MODEL_SIZES", "DEFAULT_CONFIG", "DistributedDataParallel", "ShardedDataParallel",
+           "init_distributed"]

@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("GPT2MI_LIB") or os.path.join(_HERE, "libgpt2mi.so")
 
 # the ABI these bindings are written against (include/gpt2mi.h GPT2MI_ABI_VERSION): a stale or foreign
 # library is refused at load instead of being called with the wrong argument lists
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 _c_int, _c_float, _c_size, _c_u64, _p = ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_void_p
 
@@ -26,8 +26,8 @@ _c_int, _c_float, _c_size, _c_u64, _p = ctypes.c_int, ctypes.c_float, ctypes.c_s
 _SIGS = {
     "gpt2mi_last_error": [],
     "gpt2mi_abi_version": [],
-    "gpt2mi_embed_fwd": [_p, _p, _p, _p, _c_int, _c_int, _c_int, _c_float, _c_u64, _p],
-    "gpt2mi_embed_bwd": [_p, _p, _p, _p, _c_int, _c_int, _c_int, _c_float, _c_u64, _p],
+    "gpt2mi_embed_fwd": [_p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_float, _c_u64, _p],
+    "gpt2mi_embed_bwd": [_p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_float, _c_u64, _p],
     "gpt2mi_layernorm_fwd": [_p, _p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_float, _p],
     "gpt2mi_layernorm_bwd": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_float, _c_u64, _c_int, _p],
     "gpt2mi_colsum_bf16": [_p, _p, _c_int, _c_int, _c_int, _p],
@@ -54,6 +54,15 @@ _SIGS = {
                                  _p],
     "gpt2mi_colsum_f32": [_p, _p, _c_int, _c_int, _c_int, _p],
     "gpt2mi_xent_fwd_f32": [_p, _c_int, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _p, _p, _p],
+    "gpt2mi_cast_bf16_f32": [_p, _p, _c_size, _p],
+    "gpt2mi_dlogits_accum": [_p, _c_int, _p, _c_int, _c_int, _c_int, _c_int, _c_int, _p, _c_int, _p],
+    "gpt2mi_dlogits_accum_f32": [_p, _c_int, _p, _c_int, _c_int, _c_int, _c_int, _c_int, _p, _c_int, _p],
+    "gpt2mi_branch_bwd": [_p, _p, _p, _c_int, _c_int, _c_float, _c_u64, _p],
+    "gpt2mi_branch_bwd_f32": [_p, _p, _p, _c_int, _c_int, _c_float, _c_u64, _p],
+    "gpt2mi_scale_f32": [_p, _c_size, _c_float, _p],
+    "gpt2mi_fsdp_unpack": [_p, _c_int, _p, _p, _c_size, _p],
+    "gpt2mi_fsdp_pack": [_p, _p, _c_int, _c_size, _c_size, _p],
+    "gpt2mi_fsdp_accum": [_p, _c_int, _p, _c_size, _c_int, _p],
     "gpt2mi_gemm_wgrad": [_c_int, _c_int, _c_int, _p, _c_int, _p, _c_int, _p, _c_int, _c_int, _c_float, _p, _p,
                           _c_size, _c_int, _p],
 }
@@ -123,12 +132,14 @@ EPI_BF16, EPI_F32, EPI_RESID, EPI_GELU, EPI_GELU_BWD, EPI_ATOMIC = range(6)
 FWD, DGRAD, WGRAD = 0, 1, 2
 
 
-def embed_fwd(idx, wte, wpe, x, B, T, C, p=0.0, seed=0):
-    _call("gpt2mi_embed_fwd", _ptr(idx), _ptr(wte), _ptr(wpe), _ptr(x), B, T, C, p, seed, _stream())
+def embed_fwd(idx, wte, wpe, x, B, T, C, p=0.0, seed=0, T_valid=None):
+    _call("gpt2mi_embed_fwd", _ptr(idx), _ptr(wte), _ptr(wpe), _ptr(x), B, T, T if T_valid is None else T_valid, C, p,
+          seed, _stream())
 
 
-def embed_bwd(idx, dres, dwte, dwpe, B, T, C, p=0.0, seed=0):
-    _call("gpt2mi_embed_bwd", _ptr(idx), _ptr(dres), _ptr(dwte), _ptr(dwpe), B, T, C, p, seed, _stream())
+def embed_bwd(idx, dres, dwte, dwpe, B, T, C, p=0.0, seed=0, T_valid=None):
+    _call("gpt2mi_embed_bwd", _ptr(idx), _ptr(dres), _ptr(dwte), _ptr(dwpe), B, T, T if T_valid is None else T_valid,
+          C, p, seed, _stream())
 
 
 def layernorm_fwd(x, w, b, y_bf16, y_f32, mean, rstd, M, C, eps):
@@ -215,6 +226,40 @@ def norm_partials_size() -> int:
 
 def cast_f32_bf16(x, y, n):
     _call("gpt2mi_cast_f32_bf16", _ptr(x), _ptr(y), n, _stream())
+
+
+def cast_bf16_f32(x, y, n):
+    _call("gpt2mi_cast_bf16_f32", _ptr(x), _ptr(y), n, _stream())
+
+
+def dlogits_accum(dl, ldd, g, ldg, B, Tp, Tv, V, alpha_dev=None, init=False):
+    """dl (the lm_head backward's dlogits) = alpha*dl + g over the [B, Tv, V] logits the caller saw."""
+    name = "gpt2mi_dlogits_accum_f32" if _f32(dl) else "gpt2mi_dlogits_accum"
+    if g.dtype != dl.dtype:
+        raise KernelError(f"dlogits_accum: grad dtype {g.dtype} != dlogits dtype {dl.dtype}")
+    _call(name, _ptr(dl), ldd, _ptr(g), ldg, B, Tp, Tv, V, _ptr(alpha_dev), int(init), _stream())
+
+
+def branch_bwd(dres, out, dbias, M, C, p=0.0, seed=0):
+    _call("gpt2mi_branch_bwd_f32" if _f32(out) else "gpt2mi_branch_bwd", _ptr(dres), _ptr(out), _ptr(dbias), M, C, p,
+          seed, _stream())
+
+
+def scale_(x: torch.Tensor, s: float):
+    _call("gpt2mi_scale_f32", _ptr(x), x.numel(), s, _stream())
+
+
+def fsdp_unpack(src, dst_f32, dst_bf16, n):
+    _call("gpt2mi_fsdp_unpack", _ptr(src), int(src.dtype == torch.float32), _ptr(dst_f32), _ptr(dst_bf16), n,
+          _stream())
+
+
+def fsdp_pack(src, dst, n, n_pad):
+    _call("gpt2mi_fsdp_pack", _ptr(src), _ptr(dst), int(dst.dtype == torch.float32), n, n_pad, _stream())
+
+
+def fsdp_accum(src, dst, n, accumulate=True):
+    _call("gpt2mi_fsdp_accum", _ptr(src), int(src.dtype == torch.float32), _ptr(dst), n, int(accumulate), _stream())
 
 
 def transpose_bf16(src, dst, R, C, ld_src=None, ld_dst=None):

@@ -636,6 +636,8 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dkdv_kernel(const bf16* 
 GPT2MI_EXPORT int gpt2mi_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int T, int H, int head_dim,
                                   float p_drop, uint64_t seed, void* stream) {
   GPT2MI_REQUIRE(head_dim == D, "attn_fwd: head_dim=%d (only 64 is built)", head_dim);
+  GPT2MI_REQUIRE(p_drop <= 0.f || (size_t)B * H * T * T < (1ull << 32),
+                 "attn_fwd: B*H*T*T exceeds the 32-bit dropout hash index");
   GPT2MI_REQUIRE(T % 64 == 0 && T > 0, "attn_fwd: T=%d must be a multiple of 64", T);
   GPT2MI_REQUIRE((size_t)T * 3 * H * D * sizeof(bf16) < (1ull << 31),
                  "attn_fwd: T*3C too large for the 32-bit buffer offsets of one batch row (T=%d)", T);
@@ -656,6 +658,8 @@ GPT2MI_EXPORT int gpt2mi_attn_bwd(const uint16_t* qkv, const uint16_t* out, cons
                                   float* delta, uint16_t* dqkv, float* dqkv_colsum, int B, int T, int H,
                                   int head_dim, float p_drop, uint64_t seed, void* stream) {
   GPT2MI_REQUIRE(head_dim == D, "attn_bwd: head_dim=%d (only 64 is built)", head_dim);
+  GPT2MI_REQUIRE(p_drop <= 0.f || (size_t)B * H * T * T < (1ull << 32),
+                 "attn_bwd: B*H*T*T exceeds the 32-bit dropout hash index");
   GPT2MI_REQUIRE(T % 64 == 0 && T > 0, "attn_bwd: T=%d must be a multiple of 64", T);
   GPT2MI_REQUIRE((size_t)T * 3 * H * D * sizeof(bf16) < (1ull << 31),
                  "attn_bwd: T*3C too large for the 32-bit buffer offsets of one batch row (T=%d)", T);

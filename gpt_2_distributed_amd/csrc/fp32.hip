@@ -385,6 +385,8 @@ GPT2MI_EXPORT int gpt2mi_gemm_f32(int layout, int epilogue, int M, int N, int K,
   }
   GPT2MI_REQUIRE(M > 0 && N >= 4 && N % 4 == 0 && K % FBK == 0, "gemm_f32: need N=%d %% 4 == 0 and K=%d %% 16 == 0",
                  N, K);
+  GPT2MI_REQUIRE(p_drop <= 0.f || (size_t)M * N < (1ull << 33),
+                 "gemm_f32: M*N=%zu exceeds the 32-bit dropout pair index", (size_t)M * N);
   GPT2MI_REQUIRE(layout >= 0 && layout <= 2, "gemm_f32: bad layout %d", layout);
   GPT2MI_REQUIRE(layout != 2 || M >= 4, "gemm_f32: wgrad needs M >= 4");
   GPT2MI_REQUIRE(splits >= 1 && K % (FBK * splits) == 0, "gemm_f32: K=%d must be a multiple of 16*splits(%d)", K, splits);
@@ -425,6 +427,8 @@ GPT2MI_EXPORT int gpt2mi_gemm_f32(int layout, int epilogue, int M, int N, int K,
 GPT2MI_EXPORT int gpt2mi_attn_fwd_f32(const float* qkv, float* out, float* lse, int B, int T, int H, int head_dim,
                                       float p_drop, uint64_t seed, void* stream) {
   GPT2MI_REQUIRE(head_dim == HD, "attn_fwd_f32: head_dim=%d (only 64 is built)", head_dim);
+  GPT2MI_REQUIRE(p_drop <= 0.f || (size_t)B * H * T * T < (1ull << 32),
+                 "attn_fwd_f32: B*H*T*T exceeds the 32-bit dropout hash index");
   GPT2MI_REQUIRE(T % RT == 0 && T > 0, "attn_fwd_f32: T=%d must be a multiple of 64", T);
   attn_fwd_f32_kernel<<<dim3(T / RT, B * H), kAThreads, 0, (hipStream_t)stream>>>(
       qkv, out, lse, T, H, 1.f / sqrtf((float)head_dim), seed, drop_threshold(p_drop),
@@ -436,6 +440,8 @@ GPT2MI_EXPORT int gpt2mi_attn_bwd_f32(const float* qkv, const float* out, const 
                                       float* delta, float* dqkv, float* dqkv_colsum, int B, int T, int H,
                                       int head_dim, float p_drop, uint64_t seed, void* stream) {
   GPT2MI_REQUIRE(head_dim == HD, "attn_bwd_f32: head_dim=%d (only 64 is built)", head_dim);
+  GPT2MI_REQUIRE(p_drop <= 0.f || (size_t)B * H * T * T < (1ull << 32),
+                 "attn_bwd_f32: B*H*T*T exceeds the 32-bit dropout hash index");
   GPT2MI_REQUIRE(dqkv_colsum == nullptr, "attn_bwd_f32: the fused bias-gradient partials are bf16-path only");
   GPT2MI_REQUIRE(T % RT == 0 && T > 0, "attn_bwd_f32: T=%d must be a multiple of 64", T);
   hipStream_t s = (hipStream_t)stream;

@@ -236,12 +236,22 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
 template <int VEC, int NV>
 __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restrict__ idx, const float* __restrict__ wte,
                                                         const float* __restrict__ wpe, float* __restrict__ x,
-                                                        int M, int T, int C, int nv, uint64_t seed, uint32_t thr,
-                                                        float inv_keep) {
+                                                        int M, int T, int T_valid, int C, int nv, uint64_t seed,
+                                                        uint32_t thr, float inv_keep) {
   const int lane = threadIdx.x & 63;
   for (int row = blockIdx.x * kWaves + (threadIdx.x >> 6); row < M; row += gridDim.x * kWaves) {
-    const int64_t tok = idx[row];
     const int t = row % T;
+    if (t >= T_valid) {  // sequence padding (T rounded up to the attention tile): zero rows, no table reads
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        float z[VEC];
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) z[j] = 0.f;
+        store_vec<VEC>(x + (size_t)row * C + VEC * (lane + 64 * i), z);
+      }
+      continue;
+    }
+    const int64_t tok = idx[row];
 #pragma unroll
     for (int i = 0; i < NV; ++i)
       {
@@ -262,10 +272,11 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restric
 // Embedding backward, token table: dwte[idx[m],:] += dres[m,:]*keep/(1-p) (fp32 atomics; the
 // tied lm_head wgrad has already been written into the same rows).
 __global__ __launch_bounds__(256) void embed_bwd_wte_kernel(const int64_t* __restrict__ idx, const float* __restrict__ dres,
-                                                            float* __restrict__ dwte, int M, int C, uint64_t seed,
-                                                            uint32_t thr, float inv_keep) {
+                                                            float* __restrict__ dwte, int M, int T, int T_valid, int C,
+                                                            uint64_t seed, uint32_t thr, float inv_keep) {
   const int lane = threadIdx.x & 63;
   for (int row = blockIdx.x * kWaves + (threadIdx.x >> 6); row < M; row += gridDim.x * kWaves) {
+    if (row % T >= T_valid) continue;  // padding rows carry no gradient
     const int64_t tok = idx[row];
     float* dst = dwte + (size_t)tok * C;
     const float* src = dres + (size_t)row * C;
@@ -280,10 +291,10 @@ __global__ __launch_bounds__(256) void embed_bwd_wte_kernel(const int64_t* __res
 // Embedding backward, position table: dwpe[t,c] += sum_b dres[b,t,c]*keep/(1-p). No atomics:
 // one thread per (t, c) column walks the batch.
 __global__ __launch_bounds__(256) void embed_bwd_wpe_kernel(const float* __restrict__ dres, float* __restrict__ dwpe,
-                                                            int B, int T, int C, uint64_t seed, uint32_t thr,
-                                                            float inv_keep) {
+                                                            int B, int T, int T_valid, int C, uint64_t seed,
+                                                            uint32_t thr, float inv_keep) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= T * C) return;
+  if (i >= T_valid * C) return;  // rows of wpe past T_valid are not touched (they may not exist)
   const int t = i / C, c = i % C;
   float s = 0.f;
   for (int b = 0; b < B; ++b) {
@@ -365,6 +376,8 @@ static int layernorm_bwd_t(const float* x, const float* w, const float* mean, co
                            uint64_t seed_out, int dres_init, void* stream) {
   int vec, nv;
   GPT2MI_REQUIRE(row_shape(C, &vec, &nv), "layernorm_bwd: unsupported C=%d", C);
+  GPT2MI_REQUIRE(p_out <= 0.f || (size_t)M * C < (1ull << 33),
+                 "layernorm_bwd: M*C exceeds the 32-bit dropout pair index");
   hipStream_t s = (hipStream_t)stream;
   const int g = grid_rows(M) > 2048 ? 2048 : grid_rows(M);
   const size_t sh = (size_t)kWaves * C * sizeof(float);
@@ -393,29 +406,32 @@ GPT2MI_EXPORT int gpt2mi_layernorm_bwd_f32(const float* x, const float* w, const
 }
 
 GPT2MI_EXPORT int gpt2mi_embed_fwd(const int64_t* idx, const float* wte, const float* wpe, float* x, int B, int T,
-                                   int C, float p, uint64_t seed, void* stream) {
+                                   int T_valid, int C, float p, uint64_t seed, void* stream) {
   int vec, nv;
   GPT2MI_REQUIRE(row_shape(C, &vec, &nv), "embed_fwd: unsupported C=%d", C);
+  GPT2MI_REQUIRE(T_valid > 0 && T_valid <= T, "embed_fwd: T_valid=%d not in [1, T=%d]", T_valid, T);
+  GPT2MI_REQUIRE(p <= 0.f || (size_t)B * T * C < (1ull << 33), "embed_fwd: B*T*C exceeds the 32-bit dropout pair index");
   hipStream_t s = (hipStream_t)stream;
   const int M = B * T;
   const uint32_t thr = drop_threshold(p);
   const float ik = p > 0.f ? 1.f / (1.f - p) : 1.f;
-#define X(V, N) if (vec == V && nv == N) embed_fwd_kernel<V, N><<<grid_rows(M), 256, 0, s>>>(idx, wte, wpe, x, M, T, C, nv, seed, thr, ik);
+#define X(V, N) if (vec == V && nv == N) embed_fwd_kernel<V, N><<<grid_rows(M), 256, 0, s>>>(idx, wte, wpe, x, M, T, T_valid, C, nv, seed, thr, ik);
   GPT2MI_ROW_CASES(X)
 #undef X
   return gpt2mi::check_launch("embed_fwd");
 }
 
 GPT2MI_EXPORT int gpt2mi_embed_bwd(const int64_t* idx, const float* dres, float* dwte, float* dwpe, int B, int T,
-                                   int C, float p, uint64_t seed, void* stream) {
+                                   int T_valid, int C, float p, uint64_t seed, void* stream) {
+  GPT2MI_REQUIRE(T_valid > 0 && T_valid <= T, "embed_bwd: T_valid=%d not in [1, T=%d]", T_valid, T);
   hipStream_t s = (hipStream_t)stream;
   const int M = B * T;
   const uint32_t thr = drop_threshold(p);
   const float ik = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  embed_bwd_wte_kernel<<<grid_rows(M), 256, 0, s>>>(idx, dres, dwte, M, C, seed, thr, ik);
+  embed_bwd_wte_kernel<<<grid_rows(M), 256, 0, s>>>(idx, dres, dwte, M, T, T_valid, C, seed, thr, ik);
   int rc = gpt2mi::check_launch("embed_bwd_wte");
   if (rc) return rc;
-  embed_bwd_wpe_kernel<<<(T * C + 255) / 256, 256, 0, s>>>(dres, dwpe, B, T, C, seed, thr, ik);
+  embed_bwd_wpe_kernel<<<(T_valid * C + 255) / 256, 256, 0, s>>>(dres, dwpe, B, T, T_valid, C, seed, thr, ik);
   return gpt2mi::check_launch("embed_bwd_wpe");
 }
 

@@ -90,14 +90,15 @@ __global__ __launch_bounds__(256) void xent_fwd_kernel(const TL* __restrict__ lo
     s_lse = lse;
     lse_out[row] = lse;
     const int64_t y = labels[row];
-    loss_rows[row] = (y == ignore_index) ? 0.f : lse - (float)lp[y];
+    // a label outside [0, V) (other than ignore_index) poisons its row with NaN: F.cross_entropy raises on it
+    loss_rows[row] = (y == ignore_index) ? 0.f : (y < 0 || y >= V) ? __builtin_nanf("") : lse - (float)lp[y];
   }
   __syncthreads();
   if (!dlogits) return;
-  const float lse = s_lse;
   const int64_t y = labels[row];
-  TL* dp = dlogits + (size_t)row * ldd;
   const bool ign = (y == ignore_index);
+  const float lse = (!ign && (y < 0 || y >= V)) ? __builtin_nanf("") : s_lse;
+  TL* dp = dlogits + (size_t)row * ldd;
   for (int c = 8 * tid; c < ldd; c += 8 * 256) {
     float o[8];
     if (c < V) {
@@ -170,13 +171,13 @@ __global__ __launch_bounds__(1024) void xent_row_kernel(const bf16* __restrict__
     s_bcast = lse;
     lse_out[row] = lse;
     const int64_t y = labels[row];
-    loss_rows[row] = (y == ignore_index) ? 0.f : lse - bf2f(lp[y]);
+    loss_rows[row] = (y == ignore_index) ? 0.f : (y < 0 || y >= V) ? __builtin_nanf("") : lse - bf2f(lp[y]);
   }
   __syncthreads();
   if (!dlogits) return;
-  const float lse = s_bcast;
   const int64_t y = labels[row];
   const bool ign = (y == ignore_index);
+  const float lse = (!ign && (y < 0 || y >= V)) ? __builtin_nanf("") : s_bcast;  // bad label: NaN row
   bf16* dp = dlogits + (size_t)row * ldd;
 #pragma unroll
   for (int i = 0; i < NCH; ++i) {

@@ -1,35 +1,49 @@
 """The GPT-2 training-step engine: forward -> loss -> backward as explicit HIP kernel sequences.
 
 One ``torch.autograd.Function`` wraps the whole network, so ``loss.backward()`` (the reference's
-``train_gpt2_distributed.py:412``) runs ``Engine.backward``: every gradient is produced by the
-kernels of libgpt2mi straight into the flat fp32 grad arena (``p.grad`` are views of it).
+``train_gpt2_distributed.py:412``) runs ``Engine._backward``: every gradient is produced by the
+kernels of libgpt2mi straight into the flat fp32 grad arena (``p.grad`` are views of it). The returned
+logits are differentiable too (``model.py:351`` hands them to the caller): a gradient that reaches
+them is added to the lm_head's dlogits before the lm_head backward.
+
+The sub-modules are callable on their own with the same kernels (``model.py:110-159,186-192,213-219,
+275-313``): ``GPT2Backbone.forward(idx)`` (embedding -> blocks -> ln_f), ``GPT2Block.forward(x)``,
+``MLP.forward(x)`` and ``CausalMultiHeadSelfAttention.forward(x)``, each its own autograd node whose
+backward accumulates into the same grad arena.
 
 Numerics = the reference under ``torch.autocast("cuda", bfloat16)`` (train_gpt2_distributed.py:404):
 bf16 GEMM operands with fp32 accumulation, fp32 residual stream / LayerNorm / softmax / loss,
-fp32 master weights and grads. Dropout uses the config's p (model.py:47-51) in train mode with a
-counter-based mask that backward regenerates; eval mode / p = 0 disables it.
+fp32 master weights and grads. Without autocast everything runs in fp32 (the plain model.py module).
+Dropout uses the config's p (model.py:47-51) in train mode with a counter-based mask that backward
+regenerates; eval mode / p = 0 disables it.
 
-HBM layout per (B, T) workspace (M = B*T tokens, C = n_embd, Vp = vocab padded to 128):
+Sequence lengths that are not a multiple of the 64-token attention tile are padded inside the engine
+(tokens 0, labels ignore_index, zero embedding rows): causality keeps the padding invisible to every
+real position, the loss counts real labels only, and padded rows carry exactly zero gradient.
+
+HBM layout per (B, T) workspace (M = B*T tokens, C = n_embd, Vp = vocab padded to 256):
   residual stream x[l]          fp32 [L+1][M, C]
   per block: ln1, ln2 bf16 [M,C]; mean/rstd fp32 [M]; qkv bf16 [M,3C]; attn out bf16 [M,C];
              lse fp32 [B*H,T]; x_mid fp32 [M,C]; gelu output h and dgelu = keep/(1-p)*gelu'(u) bf16 [M,4C]
-  head:      ln_f bf16 [M,C]; logits bf16 [M,Vp] (returned as a [B,T,V] view); dlogits bf16 [M,Vp]
+  head:      ln_f bf16 [M,C]; dlogits bf16 [M,Vp]; logits bf16 [M,Vp] are a FRESH tensor per forward
+             (returned as a [B,T,V] view that stays valid as long as the caller holds it)
   backward scratch: dres fp32 [M,C], dres_bf bf16 [M,C], dln bf16 [M,C], dU bf16 [M,4C],
              dqkv bf16 [M,3C], delta fp32 [B*H,T], dqkv_cs fp32 [M/32,3C]
 """
 from __future__ import annotations
 
-import math
 from dataclasses import dataclass
 from typing import Dict, List, Optional
 
 import torch
+import torch.nn.functional as F
 
 from . import _lib as K
 from ._lib import wgrad_splits as K_wgrad_splits
 
 BF16 = torch.bfloat16
 F32 = torch.float32
+ATTN_TILE = 64  # the attention kernels tile T by 64 queries / keys
 
 
 def _mix(*xs: int) -> int:
@@ -39,6 +53,10 @@ def _mix(*xs: int) -> int:
         h ^= (x + 0x9E3779B97F4A7C15 + ((h << 6) & 0xFFFFFFFFFFFFFFFF) + (h >> 2)) & 0xFFFFFFFFFFFFFFFF
         h = (h * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
     return h
+
+
+def padded_len(T: int) -> int:
+    return (T + ATTN_TILE - 1) // ATTN_TILE * ATTN_TILE
 
 
 @dataclass
@@ -56,31 +74,22 @@ class BlockActs:
     dgelu: torch.Tensor  # keep/(1-p) * gelu'(u) of the fc1 pre-activation u (from the fc1 epilogue)
     h: torch.Tensor
 
+    @staticmethod
+    def alloc(cfg, B, T, device, act, xmid=True):
+        M, C, H = B * T, cfg.n_embd, cfg.n_head
+        e = lambda *s, dt=act: torch.empty(*s, dtype=dt, device=device)  # noqa: E731
+        return BlockActs(ln1=e(M, C), m1=e(M, dt=F32), r1=e(M, dt=F32), qkv=e(M, 3 * C), ao=e(M, C),
+                         lse=e(B * H, T, dt=F32), xmid=e(M, C, dt=F32) if xmid else None, ln2=e(M, C),
+                         m2=e(M, dt=F32), r2=e(M, dt=F32), dgelu=e(M, 4 * C), h=e(M, 4 * C))
 
-class Workspace:
-    def __init__(self, cfg, B: int, T: int, vpad: int, device, act=BF16):
-        L, C, H = cfg.n_layer, cfg.n_embd, cfg.n_head
+
+class Scratch:
+    """Backward scratch of one (B, T) shape (also used by the stand-alone sub-module backwards)."""
+
+    def __init__(self, cfg, B, T, vpad, device, act, head=True):
+        C, H = cfg.n_embd, cfg.n_head
         M = B * T
         e = lambda *s, dt=act: torch.empty(*s, dtype=dt, device=device)  # noqa: E731
-        self.act = act
-        self.B, self.T, self.M = B, T, M
-        self.x = e(L + 1, M, C, dt=F32)
-        self.blocks: List[BlockActs] = []
-        for _ in range(L):
-            self.blocks.append(BlockActs(
-                ln1=e(M, C), m1=e(M, dt=F32), r1=e(M, dt=F32), qkv=e(M, 3 * C), ao=e(M, C),
-                lse=e(B * H, T, dt=F32), xmid=e(M, C, dt=F32), ln2=e(M, C), m2=e(M, dt=F32), r2=e(M, dt=F32),
-                dgelu=e(M, 4 * C), h=e(M, 4 * C)))
-        self.lnf = e(M, C)
-        self.mf = e(M, dt=F32)
-        self.rf = e(M, dt=F32)
-        self.logits = e(M, vpad)
-        self.dlogits = e(M, vpad)
-        self.loss_rows = e(M, dt=F32)
-        self.lse_ce = e(M, dt=F32)
-        self.inv_count = e(1, dt=F32)
-        self.dscale = e(1, dt=F32)
-        # backward scratch
         self.dres = e(M, C, dt=F32)
         self.dres_bf = e(M, C)
         self.dln = e(M, C)
@@ -90,10 +99,30 @@ class Workspace:
         # bf16 path: the attention backward writes 32-token partial column sums of dqkv (qkv bias grad)
         self.dqkv_cs = e(M // 32, 3 * C, dt=F32) if act == BF16 else None
         # split-K slabs of the 256x256 wgrad GEMMs
-        wshapes = [(3 * C, C), (C, C), (4 * C, C), (C, 4 * C), (vpad, C)]
+        wshapes = [(3 * C, C), (C, C), (4 * C, C), (C, 4 * C)] + ([(vpad, C)] if head else [])
         need = max((K_wgrad_splits(m, n, M) * m * n if K_wgrad_splits(m, n, M) > 1 else 0)
                    for m, n in wshapes) if C % 256 == 0 and act == BF16 else 0
         self.wgrad_ws = e(max(need, 4), dt=F32)
+
+
+class Workspace(Scratch):
+    def __init__(self, cfg, B: int, T: int, vpad: int, device, act=BF16):
+        super().__init__(cfg, B, T, vpad, device, act, head=True)
+        L, C = cfg.n_layer, cfg.n_embd
+        M = B * T
+        e = lambda *s, dt=act: torch.empty(*s, dtype=dt, device=device)  # noqa: E731
+        self.act = act
+        self.B, self.T, self.M = B, T, M
+        self.x = e(L + 1, M, C, dt=F32)
+        self.blocks: List[BlockActs] = [BlockActs.alloc(cfg, B, T, device, act) for _ in range(L)]
+        self.lnf = e(M, C)
+        self.mf = e(M, dt=F32)
+        self.rf = e(M, dt=F32)
+        self.dlogits = e(M, vpad)
+        self.loss_rows = e(M, dt=F32)
+        self.lse_ce = e(M, dt=F32)
+        self.inv_count = e(1, dt=F32)
+        self.dscale = e(1, dt=F32)
 
 
 class _NullCtxT:
@@ -123,28 +152,94 @@ class _EventCtx:
         return False
 
 
+@dataclass
+class _Saved:
+    idx: torch.Tensor          # [B, Tp] (padded)
+    labels: Optional[torch.Tensor]
+    T: int                     # caller's sequence length (<= Tp)
+    pr: float
+    pa: float
+    seeds: dict
+    act: torch.dtype
+
+
 class _GPT2Step(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, engine, idx, labels, need_grad, *params):
+    def forward(ctx, engine, idx, labels, *params):
         ctx.set_materialize_grads(False)
-        logits, loss = engine._forward(idx, labels, need_grad)
+        logits, loss = engine._forward(idx, labels, True)
         ctx.engine = engine
         ctx.token = engine._fwd_token
         ctx.n_params = len(params)
-        ctx.mark_non_differentiable(logits)
         return logits, loss
 
     @staticmethod
     def backward(ctx, grad_logits, grad_loss):
         eng = ctx.engine
-        if grad_logits is not None:
-            raise NotImplementedError("gradients through the returned logits are not supported; "
-                                      "backpropagate the returned loss")
         if ctx.token != eng._fwd_token:
             raise RuntimeError("GPT2 activations were overwritten by a later forward before this backward "
                                "(one forward/backward in flight per model)")
-        eng._backward(grad_loss)
-        return (None, None, None, None) + (None,) * ctx.n_params
+        eng._backward(grad_logits, grad_loss)
+        return (None, None, None) + (None,) * ctx.n_params
+
+
+class _TrunkFn(torch.autograd.Function):
+    """GPT2Backbone.forward(idx) (model.py:275-313): embedding -> blocks -> ln_f, fp32 output."""
+
+    @staticmethod
+    def forward(ctx, engine, idx, *params):
+        ctx.set_materialize_grads(False)
+        out = engine._trunk_forward_module(idx)
+        ctx.engine = engine
+        ctx.token = engine._fwd_token
+        ctx.n_params = len(params)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        eng = ctx.engine
+        if ctx.token != eng._fwd_token:
+            raise RuntimeError("GPT2 activations were overwritten by a later forward before this backward")
+        eng._trunk_backward_module(dy)
+        return (None, None) + (None,) * ctx.n_params
+
+
+class _SubFn(torch.autograd.Function):
+    """A stand-alone block / MLP / attention call (its own activations; grads into the arena)."""
+
+    @staticmethod
+    def forward(ctx, engine, kind, layer, x, *params):
+        ctx.set_materialize_grads(False)
+        y, state = engine._sub_forward(kind, layer, x)
+        ctx.engine, ctx.kind, ctx.layer, ctx.state, ctx.n_params = engine, kind, layer, state, len(params)
+        ctx.x_dtype = x.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dx = None
+        if dy is not None:
+            dx = ctx.engine._sub_backward(ctx.kind, ctx.layer, ctx.state, dy).to(ctx.x_dtype)
+        ctx.state = None
+        return (None, None, None, dx) + (None,) * ctx.n_params
+
+
+class GradHooks:
+    """What a data-parallel wrapper plugs into the engine (parallel.py). All no-ops here."""
+
+    def begin_backward(self) -> float:
+        """Called before any gradient is written; returns the factor every gradient of this backward is
+        scaled by (1/world for a SUM-reduced data-parallel backward)."""
+        return 1.0
+
+    def ready(self, name: str) -> None:
+        """Arena range ``name`` (parallel.ready_ranges) holds its final gradient of this backward."""
+
+    def end_backward(self) -> None:
+        """The backward's last kernel is enqueued: finish the collective before backward returns."""
+
+    def fwd_unit(self, unit: str) -> None:
+        """FSDP: the parameters of ``unit`` ("embed", "h.<l>", "head") are about to be read."""
 
 
 class Engine:
@@ -168,13 +263,16 @@ class Engine:
                            if len(sl.shape) == 2 and n != "lm_head.weight" and "wpe" not in n]
         self._shadowT_stale = True
         self._shadow_versions = None
+        self._tdesc_cache: Dict[tuple, tuple] = {}
         self._ws: Dict[tuple, Workspace] = {}
         self._fwd_token = 0
         self._step_seed = 0
         self.base_seed = 1234
-        self.grad_sync = None  # set by DDP wrappers: called as grad_sync(event, **kw)
+        self.grad_sync: Optional[GradHooks] = None  # set by data-parallel wrappers (parallel.py)
+        self.param_provider = None  # FSDP: owns the full parameter views (gathers them per unit)
+        self.grad_dirty = False     # the grad arena holds gradients of an earlier backward (accumulation)
+        self.bwd_act = F32
         self._params = list(model.parameters())
-        self._grads_bound = False
         self.params_by_name = dict(model.named_parameters())
         self.probes: Dict[str, list] = {}  # name -> [(start_event, end_event)] recorded when armed
         if not hasattr(K, "load") or self.device.type != "cuda":
@@ -190,9 +288,6 @@ class Engine:
         return _EventCtx(lst)
 
     # ---- parameter views ------------------------------------------------------------------------------
-    def _off(self, name: str) -> int:
-        return self.layout.slots[name].offset
-
     def p(self, name):  # fp32 master view
         return self.layout.view(self.model.arena, name)
 
@@ -225,30 +320,42 @@ class Engine:
         sl = self.layout.slots[name]
         return self._rows(name) % 64 == 0 and sl.shape[1] % 64 == 0
 
-    def _refresh_shadowT(self):
-        # every transposable weight in one launch (49 separate 64x64-tile launches cost 0.28 ms per step)
-        if getattr(self, "_tdesc", None) is None:
+    def refresh_shadowT(self, names=None):
+        """Transpose every (or the listed) 2-D weight of the bf16 shadow into shadowT in one launch
+        (49 separate 64x64-tile launches cost 0.28 ms per step)."""
+        key = tuple(names) if names is not None else None
+        if key not in self._tdesc_cache:
             rows, tiles = [], 0
-            for n in self._t_weights:
+            for n in (self._t_weights if names is None else [m for m in names if m in self._t_weights]):
                 if self.wT_ok(n):
                     sl = self.layout.slots[n]
                     R, Cc = self._rows(n), sl.shape[1]
                     rows.append((sl.offset, R, Cc, tiles))
                     tiles += (R // 64) * (Cc // 64)
-            self._tdesc = (torch.tensor(rows, dtype=torch.int64, device=self.device) if rows else None, len(rows),
-                           tiles)
-        desc, n, tiles = self._tdesc
+            self._tdesc_cache[key] = (torch.tensor(rows, dtype=torch.int64, device=self.device) if rows else None,
+                                      len(rows), tiles)
+        desc, n, tiles = self._tdesc_cache[key]
         if n:
             K.transpose_bf16_batched(self.shadow, self.shadowT, desc, n, tiles)
-        self._shadowT_stale = False
+        if names is None:
+            self._shadowT_stale = False
 
     def wT16(self, name):  # bf16 W^T view (flat, [in][out_padded])
         s = self.layout.slots[name]
         return self.shadowT[s.offset:s.offset + s.reserved]
 
-    def _maybe_refresh_shadow(self):
-        if self._versions() != self._shadow_versions:
-            self.refresh_shadow()
+    def _sync_shadows(self, act, need_grad):
+        if self.param_provider is not None:
+            return  # FSDP: the provider unpacks each gathered unit into the arena / shadow / shadowT
+        if act == BF16:
+            if self._versions() != self._shadow_versions:
+                self.refresh_shadow()
+            if self._shadowT_stale and need_grad:
+                self.refresh_shadowT()
+
+    def _unit(self, unit):
+        if self.param_provider is not None:
+            self.param_provider.fwd_unit(unit)
 
     # ---- grads ---------------------------------------------------------------------------------------
     def bind_grads(self):
@@ -256,16 +363,15 @@ class Engine:
             if name == "lm_head.weight":
                 continue
             p.grad = self.layout.view(self.grad, name)
-        self._grads_bound = True
 
     def zero_grad(self):
         K.zero_(self.grad)
+        self.grad_dirty = False
 
     def _prepare_grads(self):
         """Accumulate into the arena when p.grad are its views; start from zero after a
         zero_grad(set_to_none=True) (every p.grad None)."""
-        ps = [p for n, p in self.params_by_name.items()]
-        if all(p.grad is None for p in ps):
+        if all(p.grad is None for p in self.params_by_name.values()):
             self.zero_grad()
             self.bind_grads()
             return
@@ -273,6 +379,21 @@ class Engine:
             if p.grad is None or p.grad.data_ptr() != self.layout.view(self.grad, n).data_ptr():
                 raise RuntimeError(f"{n}.grad is not a view of the engine's grad arena; zero grads with "
                                    "set_to_none=True or the model's optimizer before backward")
+
+    def _begin_grads(self, act) -> float:
+        self._prepare_grads()
+        self.bwd_act = act  # the precision of this backward's gradients (FSDP reduces in it)
+        scale = self.grad_sync.begin_backward() if self.grad_sync is not None else 1.0
+        self.grad_dirty = True
+        return scale
+
+    def _ready(self, name):
+        if self.grad_sync is not None:
+            self.grad_sync.ready(name)
+
+    def _end_grads(self):
+        if self.grad_sync is not None:
+            self.grad_sync.end_backward()
 
     def workspace(self, B, T, act=BF16) -> Workspace:
         key = (B, T, act)
@@ -309,17 +430,29 @@ class Engine:
         s = self.layout.slots[name]
         return self.model.arena[s.offset:s.offset + s.reserved]
 
+    def _grad_enabled(self):
+        return torch.is_grad_enabled() and any(p.requires_grad for p in self._params)
+
     # ---- public entry -------------------------------------------------------------------------------
     def forward(self, idx: torch.Tensor, labels: Optional[torch.Tensor]):
-        need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in self._params)
-        if need_grad and labels is None:
-            need_grad = False
-        if need_grad:
-            return _GPT2Step.apply(self, idx, labels, True, *self._params)
+        if self._grad_enabled():
+            return _GPT2Step.apply(self, idx, labels, *self._params)
         with torch.no_grad():
             return self._forward(idx, labels, False)
 
-    # ---- forward ------------------------------------------------------------------------------------
+    def backbone_forward(self, idx: torch.Tensor) -> torch.Tensor:
+        if self._grad_enabled():
+            return _TrunkFn.apply(self, idx, *self._params)
+        with torch.no_grad():
+            return self._trunk_forward_module(idx)
+
+    def sub_forward(self, kind: str, layer: int, x: torch.Tensor) -> torch.Tensor:
+        if self._grad_enabled() or x.requires_grad:
+            return _SubFn.apply(self, kind, layer, x, *self._params)
+        with torch.no_grad():
+            return self._sub_forward(kind, layer, x)[0]
+
+    # ---- shared kernel sequences --------------------------------------------------------------------
     def _dropout(self):
         if not self.model.training:
             return 0.0, 0.0
@@ -333,151 +466,341 @@ class Engine:
                 s[(site, l)] = _mix(self.base_seed, step_seed, l, k + 1)
         return s
 
-    def _forward(self, idx, labels, need_grad):
-        cfg = self.cfg
-        B, T = idx.shape
-        C, H, L, V = cfg.n_embd, cfg.n_head, cfg.n_layer, cfg.vocab_size
-        Vp = self.vpad
-        M = B * T
-        if idx.dtype != torch.int64:
-            idx = idx.long()
-        idx = idx.contiguous()
-        if labels is not None:
-            labels = labels.contiguous().long()
-        act = self.compute_dtype()
-        if act == BF16:
-            self._maybe_refresh_shadow()
-            if self._shadowT_stale and need_grad:
-                self._refresh_shadowT()
-        ws = self.workspace(B, T, act)
-        W = lambda n: self.w(n, act)  # noqa: E731
-        pr, pa = self._dropout()
+    def _next_seeds(self):
         self._step_seed += 1
-        seeds = self._seeds(self._step_seed)
-        self._fwd_token += 1
-        self._saved = (idx, labels, pr, pa, seeds, act)
+        return self._seeds(self._step_seed)
 
-        x = ws.x
-        K.embed_fwd(idx, self.p("transformer.wte.weight"), self.p("transformer.wpe.weight"), x[0], B, T, C, pr,
-                    seeds["embd"])
-        for l in range(L):
-            A = ws.blocks[l]
-            pre = f"transformer.h.{l}."
-            K.layernorm_fwd(x[l], self.p(pre + "ln1.weight"), self.p(pre + "ln1.bias"), A.ln1, None, A.m1, A.r1,
-                            M, C, cfg.layer_norm_eps)
-            K.gemm(K.FWD, K.EPI_BF16, M, 3 * C, C, A.ln1, C, W(pre + "attn.qkv.weight"), C, A.qkv, 3 * C,
-                   bias=self.p(pre + "attn.qkv.bias"))
-            with self._probe("attn_fwd"):
-                K.attn_fwd(A.qkv, A.ao, A.lse, B, T, H, C // H, pa, seeds[("attn", l)])
-            K.gemm(K.FWD, K.EPI_RESID, M, C, C, A.ao, C, W(pre + "attn.proj.weight"), C, A.xmid, C,
-                   bias=self.p(pre + "attn.proj.bias"), resid=x[l], p_drop=pr, seed=seeds[("proj", l)])
-            K.layernorm_fwd(A.xmid, self.p(pre + "ln2.weight"), self.p(pre + "ln2.bias"), A.ln2, None, A.m2, A.r2,
-                            M, C, cfg.layer_norm_eps)
-            with self._probe("fc1_fwd"):
-                K.gemm(K.FWD, K.EPI_GELU, M, 4 * C, C, A.ln2, C, W(pre + "mlp.fc1.weight"), C, A.h, 4 * C,
-                       bias=self.p(pre + "mlp.fc1.bias"), aux=A.dgelu, ldaux=4 * C, p_drop=pr, seed=seeds[("fc1", l)])
-            K.gemm(K.FWD, K.EPI_RESID, M, C, 4 * C, A.h, 4 * C, W(pre + "mlp.fc2.weight"), 4 * C, x[l + 1], C,
-                   bias=self.p(pre + "mlp.fc2.bias"), resid=A.xmid, p_drop=pr, seed=seeds[("fc2", l)])
-        K.layernorm_fwd(x[L], self.p("transformer.ln_f.weight"), self.p("transformer.ln_f.bias"), ws.lnf, None,
-                        ws.mf, ws.rf, M, C, cfg.layer_norm_eps)
-        with self._probe("lm_head_fwd"):
-            K.gemm(K.FWD, K.EPI_BF16, M, Vp, C, ws.lnf, C, W("transformer.wte.weight"), C, ws.logits, Vp)
-        loss = None
-        if labels is not None:
-            loss = torch.empty((), dtype=F32, device=self.device)  # fresh: callers may keep it across steps
-            K.xent_fwd(ws.logits, Vp, labels, ws.loss_rows, ws.lse_ce, ws.dlogits if need_grad else None, Vp, M, V,
-                       loss, ws.inv_count)
-        logits = ws.logits.view(B, T, Vp)[:, :, :V]
-        return logits, loss
-
-    # ---- backward -----------------------------------------------------------------------------------
-    def _backward(self, grad_loss: torch.Tensor):
+    def _ln_fwd(self, x, pre, out, mean, rstd, M, out_f32=None):
         cfg = self.cfg
-        idx, labels, pr, pa, seeds, act = self._saved
-        B, T = idx.shape
-        C, H, L = cfg.n_embd, cfg.n_head, cfg.n_layer
-        Vp = self.vpad
+        K.layernorm_fwd(x, self.p(pre + ".weight"), self.p(pre + ".bias"), out, None, mean, rstd, M, cfg.n_embd,
+                        cfg.layer_norm_eps)
+        if out_f32 is not None:  # the fp32 copy a stand-alone Backbone returns (autocast LN output is fp32)
+            K.layernorm_fwd(x, self.p(pre + ".weight"), self.p(pre + ".bias"), None, out_f32, mean, rstd, M,
+                            cfg.n_embd, cfg.layer_norm_eps)
+
+    def _attn_fwd(self, l, A, resid, out, B, T, act, pr, pa, seeds):
+        """A.ln1 -> qkv GEMM -> flash attention -> proj GEMM: out = resid + drop(proj(attn))."""
+        C, H = self.cfg.n_embd, self.cfg.n_head
         M = B * T
-        ws = self.workspace(B, T, act)
-        W = lambda n: self.w(n, act)  # noqa: E731
-        self._prepare_grads()
-        if grad_loss is None:
-            return
-        grad_loss = grad_loss.reshape(1).to(F32)
-        K.scale_mul(grad_loss, ws.inv_count, ws.dscale)  # d(loss)/d(logit) scale = grad / #valid
-        sync = self.grad_sync
-        S = self.WGRAD_SPLITS
-        while S > 1 and M % (64 * S) != 0:
-            S //= 2
+        pre = f"transformer.h.{l}."
+        K.gemm(K.FWD, K.EPI_BF16, M, 3 * C, C, A.ln1, C, self.w(pre + "attn.qkv.weight", act), C, A.qkv, 3 * C,
+               bias=self.p(pre + "attn.qkv.bias"))
+        with self._probe("attn_fwd"):
+            K.attn_fwd(A.qkv, A.ao, A.lse, B, T, H, C // H, pa, seeds[("attn", l)])
+        K.gemm(K.FWD, K.EPI_RESID, M, C, C, A.ao, C, self.w(pre + "attn.proj.weight", act), C, out, C,
+               bias=self.p(pre + "attn.proj.bias"), resid=resid, p_drop=pr, seed=seeds[("proj", l)])
 
-        def wgrad(m, n, a, lda, b, ldb, out):
-            # dW[m][n] += dY[:, :m]^T X[:, :n] over the M tokens
-            if act == F32:
-                K.gemm(K.WGRAD, K.EPI_F32, m, n, M, a, lda, b, ldb, out, n, accumulate=True)
-            elif m % 256 == 0 and n % 256 == 0:
-                K.gemm_wgrad(m, n, M, a, lda, b, ldb, out, n, accumulate=True, workspace=ws.wgrad_ws,
-                             splits=K_wgrad_splits(m, n, M))
-            else:
-                K.gemm(K.WGRAD, K.EPI_ATOMIC, m, n, M, a, lda, b, ldb, out, n, splits=S)
+    def _mlp_fwd(self, l, A, resid, out, M, act, pr, seeds):
+        """A.ln2 -> fc1 GEMM + GELU + drop1 (also the masked GELU derivative) -> fc2 GEMM: out = resid + drop2(.)."""
+        C = self.cfg.n_embd
+        pre = f"transformer.h.{l}."
+        with self._probe("fc1_fwd"):
+            K.gemm(K.FWD, K.EPI_GELU, M, 4 * C, C, A.ln2, C, self.w(pre + "mlp.fc1.weight", act), C, A.h, 4 * C,
+                   bias=self.p(pre + "mlp.fc1.bias"), aux=A.dgelu, ldaux=4 * C, p_drop=pr, seed=seeds[("fc1", l)])
+        K.gemm(K.FWD, K.EPI_RESID, M, C, 4 * C, A.h, 4 * C, self.w(pre + "mlp.fc2.weight", act), 4 * C, out, C,
+               bias=self.p(pre + "mlp.fc2.bias"), resid=resid, p_drop=pr, seed=seeds[("fc2", l)])
+
+    def _block_fwd(self, l, A, x_in, x_out, B, T, act, pr, pa, seeds):
+        M = B * T
+        pre = f"transformer.h.{l}."
+        self._ln_fwd(x_in, pre + "ln1", A.ln1, A.m1, A.r1, M)
+        self._attn_fwd(l, A, x_in, A.xmid, B, T, act, pr, pa, seeds)
+        self._ln_fwd(A.xmid, pre + "ln2", A.ln2, A.m2, A.r2, M)
+        self._mlp_fwd(l, A, A.xmid, x_out, M, act, pr, seeds)
+
+    def _trunk_fwd(self, ws, idx, B, T, T_valid, act, pr, pa, seeds, lnf_f32=None):
+        C, L = self.cfg.n_embd, self.cfg.n_layer
         x = ws.x
+        self._unit("embed")
+        K.embed_fwd(idx, self.p("transformer.wte.weight"), self.p("transformer.wpe.weight"), x[0], B, T, C, pr,
+                    seeds["embd"], T_valid=T_valid)
+        for l in range(L):
+            self._unit(f"h.{l}")
+            self._block_fwd(l, ws.blocks[l], x[l], x[l + 1], B, T, act, pr, pa, seeds)
+        self._unit("head")
+        self._ln_fwd(x[L], "transformer.ln_f", ws.lnf, ws.mf, ws.rf, B * T, out_f32=lnf_f32)
 
-        def dgrad(out, dy, wname, n_in, n_out, epi=K.EPI_BF16, **kw):
-            # dX[M][n_in] = dY[M][n_out] . W[n_out][n_in]: the forward layout against W^T when it exists
-            if act == BF16 and self.wT_ok(wname):
-                K.gemm(K.FWD, epi, M, n_in, n_out, dy, n_out, self.wT16(wname), n_out, out, n_in, **kw)
-            else:
-                K.gemm(K.DGRAD, epi, M, n_in, n_out, dy, n_out, W(wname), n_in, out, n_in, **kw)
+    # -- backward pieces. The data-parallel 1/world factor (GradHooks.begin_backward) enters once, with the
+    # gradient that starts the backward (the lm_head dgrad/wgrad alpha, or the incoming dy): every op
+    # below is linear in it, so no GEMM here needs a scale. --
+    def _wgrad(self, S, act, m, n, M, a, lda, b, ldb, out):
+        # dW[m][n] += dY[:, :m]^T X[:, :n] over the M tokens
+        if act == F32:
+            K.gemm(K.WGRAD, K.EPI_F32, m, n, M, a, lda, b, ldb, out, n, accumulate=True)
+        elif m % 256 == 0 and n % 256 == 0:
+            K.gemm_wgrad(m, n, M, a, lda, b, ldb, out, n, accumulate=True, workspace=S.wgrad_ws,
+                         splits=K_wgrad_splits(m, n, M))
+        else:
+            s = self.WGRAD_SPLITS
+            while s > 1 and M % (64 * s) != 0:
+                s //= 2
+            K.gemm(K.WGRAD, K.EPI_ATOMIC, m, n, M, a, lda, b, ldb, out, n, splits=s)
 
-        # lm_head (tied): dlnf = dlogits @ wte ; dwte (+)= dlogits^T @ lnf
-        with self._probe("lm_head_dgrad"):
-            dgrad(ws.dln, ws.dlogits, "transformer.wte.weight", C, Vp, K.EPI_BF16, alpha_dev=ws.dscale)
-        wte_g = self.layout.padded_view(self.grad, "transformer.wte.weight", Vp)
-        with self._probe("lm_head_wgrad"):
-            if C % 256 == 0 and act == BF16:
-                K.gemm_wgrad(Vp, C, M, ws.dlogits, Vp, ws.lnf, C, wte_g, C, accumulate=True, alpha_dev=ws.dscale,
-                             workspace=ws.wgrad_ws, splits=K_wgrad_splits(Vp, C, M))
-            else:
-                K.gemm(K.WGRAD, K.EPI_F32, Vp, C, M, ws.dlogits, Vp, ws.lnf, C, wte_g, C, alpha_dev=ws.dscale,
-                       accumulate=True)
+    def _dgrad(self, act, M, out, dy, wname, n_in, n_out, epi=K.EPI_BF16, **kw):
+        # dX[M][n_in] = dY[M][n_out] . W[n_out][n_in]: the forward layout against W^T when it exists
+        if act == BF16 and self.wT_ok(wname):
+            K.gemm(K.FWD, epi, M, n_in, n_out, dy, n_out, self.wT16(wname), n_out, out, n_in, **kw)
+        else:
+            K.gemm(K.DGRAD, epi, M, n_in, n_out, dy, n_out, self.w(wname, act), n_in, out, n_in, **kw)
+
+    def _mlp_bwd(self, l, A, S, dY, dx_out, M, act):
+        """dY = grad of the fc2 output with drop2 applied (its bias grad already taken) -> dx_out = grad of
+        the MLP input (bf16), weight grads of fc1/fc2 and the fc1 bias grad."""
+        C = self.cfg.n_embd
+        pre = f"transformer.h.{l}."
+        self._dgrad(act, M, S.dU, dY, pre + "mlp.fc2.weight", 4 * C, C, K.EPI_GELU_BWD, aux=A.dgelu, ldaux=4 * C,
+                    dbias=self.g(pre + "mlp.fc1.bias"))
+        self._wgrad(S, act, C, 4 * C, M, dY, C, A.h, 4 * C, self.g(pre + "mlp.fc2.weight"))
+        self._dgrad(act, M, dx_out, S.dU, pre + "mlp.fc1.weight", C, 4 * C)
+        self._wgrad(S, act, 4 * C, C, M, S.dU, 4 * C, A.ln2, C, self.g(pre + "mlp.fc1.weight"))
+
+    def _attn_bwd(self, l, A, S, dY, dx_out, B, T, act, pa, seeds):
+        """dY = grad of the proj output with resid_drop applied -> dx_out = grad of the attention input."""
+        C, H = self.cfg.n_embd, self.cfg.n_head
+        M = B * T
+        pre = f"transformer.h.{l}."
+        self._dgrad(act, M, dx_out, dY, pre + "attn.proj.weight", C, C)
+        self._wgrad(S, act, C, C, M, dY, C, A.ao, C, self.g(pre + "attn.proj.weight"))
+        K.attn_bwd(A.qkv, A.ao, dx_out, A.lse, S.delta, S.dqkv, B, T, H, C // H, pa, seeds[("attn", l)],
+                   colsum=S.dqkv_cs)
+        self._dgrad(act, M, dx_out, S.dqkv, pre + "attn.qkv.weight", C, 3 * C)
+        self._wgrad(S, act, 3 * C, C, M, S.dqkv, 3 * C, A.ln1, C, self.g(pre + "attn.qkv.weight"))
+        if S.dqkv_cs is not None:  # qkv bias grad: sum the attention backward's 32-token partials
+            K.colsum_bf16(S.dqkv_cs, self.g(pre + "attn.qkv.bias"), M // 32, 3 * C, 3 * C)
+        else:
+            K.colsum_bf16(S.dqkv, self.g(pre + "attn.qkv.bias"), M, 3 * C, 3 * C)
+
+    def _block_bwd(self, l, A, S, x_in, B, T, act, pr, pa, seeds, last):
+        """S.dres = grad of the block output; S.dres_bf = its fc2 branch grad (drop2 applied) ->
+        S.dres = grad of the block input; unless `last`, S.dres_bf = the fc2 branch grad of block l-1."""
+        C = self.cfg.n_embd
+        M = B * T
+        pre = f"transformer.h.{l}."
+        self._mlp_bwd(l, A, S, S.dres_bf, S.dln, M, act)
+        K.layernorm_bwd(A.xmid, self.p(pre + "ln2.weight"), A.m2, A.r2, S.dln, S.dres, self.g(pre + "ln2.weight"),
+                        self.g(pre + "ln2.bias"), S.dres_bf, self.g(pre + "attn.proj.bias"), M, C, pr,
+                        seeds[("proj", l)])
+        self._attn_bwd(l, A, S, S.dres_bf, S.dln, B, T, act, pa, seeds)
+        if not last:
+            K.layernorm_bwd(x_in, self.p(pre + "ln1.weight"), A.m1, A.r1, S.dln, S.dres,
+                            self.g(pre + "ln1.weight"), self.g(pre + "ln1.bias"), S.dres_bf,
+                            self.g(f"transformer.h.{l-1}.mlp.fc2.bias"), M, C, pr, seeds[("fc2", l - 1)])
+        else:
+            K.layernorm_bwd(x_in, self.p(pre + "ln1.weight"), A.m1, A.r1, S.dln, S.dres,
+                            self.g(pre + "ln1.weight"), self.g(pre + "ln1.bias"), None, None, M, C)
+
+    def _trunk_bwd(self, ws, sv: _Saved):
+        """ws.dln = grad of the ln_f output -> every trunk gradient (ln_f, blocks, embeddings)."""
+        C, L = self.cfg.n_embd, self.cfg.n_layer
+        idx, pr, pa, seeds, act = sv.idx, sv.pr, sv.pa, sv.seeds, sv.act
+        B, T = idx.shape
+        M = B * T
+        x = ws.x
         # ln_f backward starts the residual gradient; emits the fc2 branch grad of the last block
         K.layernorm_bwd(x[L], self.p("transformer.ln_f.weight"), ws.mf, ws.rf, ws.dln, ws.dres,
                         self.g("transformer.ln_f.weight"), self.g("transformer.ln_f.bias"), ws.dres_bf,
                         self.g(f"transformer.h.{L-1}.mlp.fc2.bias"), M, C, pr, seeds[("fc2", L - 1)], dres_init=True)
-        if sync:
-            sync("ready", name="transformer.ln_f.bias")
+        self._ready("head")
         for l in reversed(range(L)):
-            A = ws.blocks[l]
-            pre = f"transformer.h.{l}."
-            # ---- MLP: dY2 = dres_bf (fc2 dropout applied), db2 done by the LN bwd above
-            dgrad(ws.dU, ws.dres_bf, pre + "mlp.fc2.weight", 4 * C, C, K.EPI_GELU_BWD, aux=A.dgelu, ldaux=4 * C,
-                  dbias=self.g(pre + "mlp.fc1.bias"))
-            wgrad(C, 4 * C, ws.dres_bf, C, A.h, 4 * C, self.g(pre + "mlp.fc2.weight"))
-            dgrad(ws.dln, ws.dU, pre + "mlp.fc1.weight", C, 4 * C)
-            wgrad(4 * C, C, ws.dU, 4 * C, A.ln2, C, self.g(pre + "mlp.fc1.weight"))
-            K.layernorm_bwd(A.xmid, self.p(pre + "ln2.weight"), A.m2, A.r2, ws.dln, ws.dres, self.g(pre + "ln2.weight"),
-                            self.g(pre + "ln2.bias"), ws.dres_bf, self.g(pre + "attn.proj.bias"), M, C, pr,
-                            seeds[("proj", l)])
-            # ---- attention
-            dgrad(ws.dln, ws.dres_bf, pre + "attn.proj.weight", C, C)
-            wgrad(C, C, ws.dres_bf, C, A.ao, C, self.g(pre + "attn.proj.weight"))
-            K.attn_bwd(A.qkv, A.ao, ws.dln, A.lse, ws.delta, ws.dqkv, B, T, H, C // H, pa, seeds[("attn", l)],
-                       colsum=ws.dqkv_cs)
-            dgrad(ws.dln, ws.dqkv, pre + "attn.qkv.weight", C, 3 * C)
-            wgrad(3 * C, C, ws.dqkv, 3 * C, A.ln1, C, self.g(pre + "attn.qkv.weight"))
-            if ws.dqkv_cs is not None:  # qkv bias grad: sum the attention backward's 32-token partials
-                K.colsum_bf16(ws.dqkv_cs, self.g(pre + "attn.qkv.bias"), M // 32, 3 * C, 3 * C)
-            else:
-                K.colsum_bf16(ws.dqkv, self.g(pre + "attn.qkv.bias"), M, 3 * C, 3 * C)
-            if l > 0:
-                K.layernorm_bwd(x[l], self.p(pre + "ln1.weight"), A.m1, A.r1, ws.dln, ws.dres,
-                                self.g(pre + "ln1.weight"), self.g(pre + "ln1.bias"), ws.dres_bf,
-                                self.g(f"transformer.h.{l-1}.mlp.fc2.bias"), M, C, pr, seeds[("fc2", l - 1)])
-            else:
-                K.layernorm_bwd(x[l], self.p(pre + "ln1.weight"), A.m1, A.r1, ws.dln, ws.dres,
-                                self.g(pre + "ln1.weight"), self.g(pre + "ln1.bias"), None, None, M, C)
-            if sync:
-                sync("ready", name=pre + "ln1.weight")
+            self._block_bwd(l, ws.blocks[l], ws, x[l], B, T, act, pr, pa, seeds, last=(l == 0))
+            self._ready(f"h.{l}")
+        # embedding backward: atomics into the tied wte grad (the lm_head wgrad already wrote it)
         K.embed_bwd(idx, ws.dres, self.g("transformer.wte.weight"), self.g("transformer.wpe.weight"), B, T, C, pr,
-                    seeds["embd"])
-        if sync:
-            sync("ready", name="transformer.wte.weight")
+                    seeds["embd"], T_valid=sv.T)
+        self._ready("embed")
+
+    # ---- the whole step ------------------------------------------------------------------------------
+    def _pad(self, idx, labels):
+        B, T = idx.shape
+        if idx.dtype != torch.int64:
+            idx = idx.long()
+        idx = idx.contiguous()
+        if labels is not None:
+            if labels.shape != idx.shape:
+                raise ValueError(f"labels shape {tuple(labels.shape)} != idx shape {tuple(idx.shape)}")
+            labels = labels.contiguous().long()
+        Tp = padded_len(T)
+        if Tp != T:  # pad to the attention tile: token 0, label ignore_index, zero embedding rows
+            idx = F.pad(idx, (0, Tp - T))
+            if labels is not None:
+                labels = F.pad(labels, (0, Tp - T), value=-100)
+        return idx, labels, T
+
+    def _forward(self, idx, labels, need_grad):
+        cfg = self.cfg
+        V, Vp, C = cfg.vocab_size, self.vpad, cfg.n_embd
+        idx, labels, T = self._pad(idx, labels)
+        B, Tp = idx.shape
+        M = B * Tp
+        act = self.compute_dtype()
+        self._sync_shadows(act, need_grad)
+        ws = self.workspace(B, Tp, act)
+        pr, pa = self._dropout()
+        seeds = self._next_seeds()
+        self._fwd_token += 1
+        self._saved = _Saved(idx, labels, T, pr, pa, seeds, act)
+        self._trunk_fwd(ws, idx, B, Tp, T, act, pr, pa, seeds)
+        logits = torch.empty(M, Vp, dtype=act, device=self.device)  # fresh: the caller may keep it
+        with self._probe("lm_head_fwd"):
+            K.gemm(K.FWD, K.EPI_BF16, M, Vp, C, ws.lnf, C, self.w("transformer.wte.weight", act), C, logits, Vp)
+        loss = None
+        if labels is not None:
+            loss = torch.empty((), dtype=F32, device=self.device)  # fresh: callers may keep it across steps
+            K.xent_fwd(logits, Vp, labels, ws.loss_rows, ws.lse_ce, ws.dlogits if need_grad else None, Vp, M, V,
+                       loss, ws.inv_count)
+        return logits.view(B, Tp, Vp)[:, :T, :V], loss
+
+    def _backward(self, grad_logits, grad_loss):
+        cfg = self.cfg
+        sv = self._saved
+        B, Tp = sv.idx.shape
+        C, V, Vp = cfg.n_embd, cfg.vocab_size, self.vpad
+        M = B * Tp
+        act = sv.act
+        ws = self.workspace(B, Tp, act)
+        use_loss = grad_loss is not None and sv.labels is not None
+        if not use_loss and grad_logits is None:
+            self._prepare_grads()
+            return
+        gs = self._begin_grads(act)
+        alpha_dev = None
+        if use_loss:  # d(loss)/d(logit) = grad_loss / #valid labels times the unscaled dlogits
+            K.scale_mul(grad_loss.reshape(1).to(F32), ws.inv_count, ws.dscale)
+            alpha_dev = ws.dscale
+        if grad_logits is not None:  # a loss on the returned logits: dlogits = alpha*dlogits + g
+            g = grad_logits.to(act).contiguous()
+            K.dlogits_accum(ws.dlogits, Vp, g, V, B, Tp, sv.T, V, alpha_dev=alpha_dev, init=not use_loss)
+            alpha_dev = None
+        # lm_head (tied): dlnf = gs * dlogits @ wte ; dwte (+)= gs * dlogits^T @ lnf
+        with self._probe("lm_head_dgrad"):
+            self._dgrad(act, M, ws.dln, ws.dlogits, "transformer.wte.weight", C, Vp, K.EPI_BF16, alpha_dev=alpha_dev,
+                        alpha=gs)
+        wte_g = self.layout.padded_view(self.grad, "transformer.wte.weight", Vp)
+        with self._probe("lm_head_wgrad"):
+            if C % 256 == 0 and act == BF16:
+                K.gemm_wgrad(Vp, C, M, ws.dlogits, Vp, ws.lnf, C, wte_g, C, accumulate=True, alpha_dev=alpha_dev,
+                             alpha=gs, workspace=ws.wgrad_ws, splits=K_wgrad_splits(Vp, C, M))
+            else:
+                K.gemm(K.WGRAD, K.EPI_F32, Vp, C, M, ws.dlogits, Vp, ws.lnf, C, wte_g, C, alpha_dev=alpha_dev,
+                       alpha=gs, accumulate=True)
+        self._trunk_bwd(ws, sv)
+        self._end_grads()
+
+    # ---- GPT2Backbone.forward on its own -------------------------------------------------------------
+    def _trunk_forward_module(self, idx):
+        idx, _, T = self._pad(idx, None)
+        B, Tp = idx.shape
+        act = self.compute_dtype()
+        self._sync_shadows(act, self._grad_enabled())
+        ws = self.workspace(B, Tp, act)
+        pr, pa = self._dropout()
+        seeds = self._next_seeds()
+        self._fwd_token += 1
+        self._saved = _Saved(idx, None, T, pr, pa, seeds, act)
+        out = torch.empty(B * Tp, self.cfg.n_embd, dtype=F32, device=self.device)
+        self._trunk_fwd(ws, idx, B, Tp, T, act, pr, pa, seeds, lnf_f32=out)
+        return out.view(B, Tp, -1)[:, :T]
+
+    def _trunk_backward_module(self, dy):
+        sv = self._saved
+        B, Tp = sv.idx.shape
+        C = self.cfg.n_embd
+        ws = self.workspace(B, Tp, sv.act)
+        gs = self._begin_grads(sv.act)
+        dy = dy.to(F32)
+        if Tp != sv.T:
+            dy = F.pad(dy, (0, 0, 0, Tp - sv.T))
+        dy = (dy * gs if gs != 1.0 else dy).contiguous()
+        if sv.act == BF16:
+            K.cast_f32_bf16(dy, ws.dln, B * Tp * C)
+        else:
+            ws.dln.copy_(dy.view(B * Tp, C))
+        self._trunk_bwd(ws, sv)
+        self._end_grads()
+
+    # ---- GPT2Block / MLP / CausalMultiHeadSelfAttention forward on their own --------------------------
+    def _sub_forward(self, kind, l, x):
+        """kind: "block" (x = residual stream, model.py:213-219), "mlp" (x = ln2 output, model.py:186-192),
+        "attn" (x = ln1 output, model.py:110-159). Returns (y, saved state)."""
+        cfg = self.cfg
+        C = cfg.n_embd
+        if x.dim() != 3 or x.shape[-1] != C:
+            raise ValueError(f"expected x of shape [B, T, {C}], got {tuple(x.shape)}")
+        if not x.is_cuda:
+            raise RuntimeError("the MI355X sub-module kernels take cuda tensors (there is no CPU fallback)")
+        B, T, _ = x.shape
+        if kind == "attn" and T > cfg.n_positions:
+            raise ValueError(f"Sequence length {T} > model max {cfg.n_positions}")
+        Tp = padded_len(T)
+        M = B * Tp
+        act = self.compute_dtype()
+        self._sync_shadows(act, self._grad_enabled())
+        xf = x.to(F32)
+        if Tp != T:
+            xf = F.pad(xf, (0, 0, 0, Tp - T))
+        xf = xf.contiguous().view(M, C)
+        pr, pa = self._dropout()
+        seeds = self._next_seeds()
+        self.last_seeds = seeds
+        A = BlockActs.alloc(cfg, B, Tp, self.device, act, xmid=(kind == "block"))
+        y = torch.empty(M, C, dtype=F32, device=self.device)
+        self._unit(f"h.{l}")
+        if kind == "block":
+            self._block_fwd(l, A, xf, y, B, Tp, act, pr, pa, seeds)
+        else:
+            zero = torch.zeros(M, C, dtype=F32, device=self.device)
+            if kind == "mlp":
+                A.ln2 = self._to_act(xf, act)
+                self._mlp_fwd(l, A, zero, y, M, act, pr, seeds)
+            elif kind == "attn":
+                A.ln1 = self._to_act(xf, act)
+                self._attn_fwd(l, A, zero, y, B, Tp, act, pr, pa, seeds)
+            else:
+                raise ValueError(kind)
+        state = (A, xf, B, Tp, T, act, pr, pa, seeds)
+        out = y.view(B, Tp, C)[:, :T]
+        if kind != "block":  # the branch output is a linear's output: bf16 under autocast (model.py:158,191)
+            out = out.to(act)
+        return out, state
+
+    @staticmethod
+    def _to_act(xf, act):
+        if act == F32:
+            return xf
+        out = torch.empty(xf.shape, dtype=BF16, device=xf.device)
+        K.cast_f32_bf16(xf, out, xf.numel())
+        return out
+
+    def _sub_backward(self, kind, l, state, dy):
+        A, xf, B, Tp, T, act, pr, pa, seeds = state
+        C = self.cfg.n_embd
+        M = B * Tp
+        S = Scratch(self.cfg, B, Tp, self.vpad, self.device, act, head=False)
+        gs = self._begin_grads(act)
+        d = dy.to(F32)
+        if Tp != T:
+            d = F.pad(d, (0, 0, 0, Tp - T))
+        S.dres.copy_(d.reshape(M, C))
+        if gs != 1.0:
+            K.scale_(S.dres, gs)
+        pre = f"transformer.h.{l}."
+        if kind == "block":
+            K.branch_bwd(S.dres, S.dres_bf, self.g(pre + "mlp.fc2.bias"), M, C, pr, seeds[("fc2", l)])
+            self._block_bwd(l, A, S, xf, B, Tp, act, pr, pa, seeds, last=True)
+            dx = S.dres
+        else:
+            site, bias = ("fc2", "mlp.fc2.bias") if kind == "mlp" else ("proj", "attn.proj.bias")
+            K.branch_bwd(S.dres, S.dres_bf, self.g(pre + bias), M, C, pr, seeds[(site, l)])
+            if kind == "mlp":
+                self._mlp_bwd(l, A, S, S.dres_bf, S.dln, M, act)
+            else:
+                self._attn_bwd(l, A, S, S.dres_bf, S.dln, B, Tp, act, pa, seeds)
+            if act == BF16:
+                dx = torch.empty(M, C, dtype=F32, device=self.device)
+                K.cast_bf16_f32(S.dln, dx, M * C)
+            else:
+                dx = S.dln
+        if gs != 1.0:  # the grads were formed from gs*dy; the input grad leaves the node unscaled
+            dx = dx / gs
+        self._end_grads()
+        return dx.view(B, Tp, C)[:, :T]

@@ -19,12 +19,17 @@ What differs underneath (MI355X-first):
   reference module (fp32 MFMA GEMMs, fp32 attention). ``model.precision = "bf16" | "fp32"``
   overrides the autocast-following default ``"auto"``;
 * no [T,T] ``mask`` buffer (model.py:105-108): causality comes from tile indices (the buffer was
-  non-persistent, so state_dicts are unchanged).
+  non-persistent, so state_dicts are unchanged);
+* the sub-modules of a GPT2 are callable on their own (``GPT2Backbone.forward(idx)`` -> ln_f output,
+  ``GPT2Block.forward(x)``, ``MLP.forward(x)``, ``CausalMultiHeadSelfAttention.forward(x)``) and
+  differentiable, through the same kernels; they read the parameters from the owning GPT2's arena, so a
+  block constructed outside a GPT2 has no MI355X path (it raises).
 The GPU path has no CPU fallback: a CPU ``forward`` raises.
 """
 from __future__ import annotations
 
 import math
+import weakref
 from dataclasses import dataclass
 from typing import Optional, Tuple
 
@@ -63,8 +68,28 @@ class NewGELU(nn.Module):
         return 0.5 * input * (1.0 + torch.tanh(math.sqrt(2.0 / math.pi) * (input + 0.044715 * torch.pow(input, 3.0))))
 
 
-class CausalMultiHeadSelfAttention(nn.Module):
-    """Parameter container mirroring model.py:80-159 (qkv, proj, two dropouts)."""
+class _OwnedByGPT2:
+    """Sub-modules of a GPT2 run through the owner's engine (parameters live in its flat arena)."""
+
+    def _bind_owner(self, owner: "GPT2", layer: Optional[int]):
+        self._owner_ref = weakref.ref(owner)
+        self._layer = layer
+
+    def _owner_engine(self):
+        ref = getattr(self, "_owner_ref", None)
+        owner = ref() if ref is not None else None
+        if owner is None:
+            raise RuntimeError(f"{type(self).__name__} runs on the MI355X engine only as a sub-module of a GPT2 "
+                               "model (its parameters live in the GPT2's flat arena)")
+        if not owner.arena.is_cuda:
+            raise RuntimeError("gpt_2_distributed_amd runs only on the MI355X HIP path: move the model to a cuda "
+                               "device (there is no CPU fallback)")
+        return owner.engine()
+
+
+class CausalMultiHeadSelfAttention(_OwnedByGPT2, nn.Module):
+    """Causal multi-head self-attention (model.py:80-159): qkv, proj, attn/resid dropout. ``forward(x)``
+    takes the ln1 output [B,T,C] and returns drop(proj(attention)) (bf16 under autocast)."""
 
     def __init__(self, cfg: GPT2Config):
         super().__init__()
@@ -77,11 +102,12 @@ class CausalMultiHeadSelfAttention(nn.Module):
         self.resid_drop = nn.Dropout(cfg.resid_pdrop)
 
     def forward(self, x):
-        raise NotImplementedError("blocks run fused inside GPT2.forward (one HIP kernel sequence)")
+        return self._owner_engine().sub_forward("attn", self._layer, x)
 
 
-class MLP(nn.Module):
-    """Parameter container mirroring model.py:162-192 (fc1, fc2, NewGELU, drop1, drop2)."""
+class MLP(_OwnedByGPT2, nn.Module):
+    """MLP (model.py:162-192): fc1 -> NewGELU -> drop1 -> fc2 -> drop2. ``forward(x)`` takes the ln2
+    output [B,T,C] (bf16 under autocast)."""
 
     def __init__(self, cfg: GPT2Config):
         super().__init__()
@@ -93,11 +119,12 @@ class MLP(nn.Module):
         self.drop2 = nn.Dropout(cfg.resid_pdrop)
 
     def forward(self, x):
-        raise NotImplementedError("blocks run fused inside GPT2.forward (one HIP kernel sequence)")
+        return self._owner_engine().sub_forward("mlp", self._layer, x)
 
 
-class GPT2Block(nn.Module):
-    """One transformer block (model.py:195-219); the unit the FSDP mode shards by."""
+class GPT2Block(_OwnedByGPT2, nn.Module):
+    """One transformer block (model.py:195-219); the unit the FSDP mode shards by. ``forward(x)``:
+    x + attn(ln1(x)), then x + mlp(ln2(x)) on the fp32 residual stream [B,T,C]."""
 
     def __init__(self, cfg: GPT2Config):
         super().__init__()
@@ -107,10 +134,10 @@ class GPT2Block(nn.Module):
         self.mlp = MLP(cfg)
 
     def forward(self, x):
-        raise NotImplementedError("blocks run fused inside GPT2.forward (one HIP kernel sequence)")
+        return self._owner_engine().sub_forward("block", self._layer, x)
 
 
-class GPT2Backbone(nn.Module):
+class GPT2Backbone(_OwnedByGPT2, nn.Module):
     """Embeddings + blocks + ln_f (model.py:225-313), same init (model.py:249-268)."""
 
     def __init__(self, cfg: GPT2Config):
@@ -136,7 +163,15 @@ class GPT2Backbone(nn.Module):
         return self.cfg.n_positions
 
     def forward(self, idx: torch.Tensor) -> torch.Tensor:
-        raise NotImplementedError("call GPT2.forward; the backbone runs fused with the lm_head")
+        """Embeddings -> blocks -> ln_f (model.py:275-313); returns the fp32 ln_f output [B,T,C]."""
+        B, T = idx.size()
+        if T > self.cfg.n_positions:
+            raise ValueError(f"Sequence length {T} > model max {self.cfg.n_positions}")
+        eng = self._owner_engine()
+        if not idx.is_cuda:
+            raise RuntimeError("gpt_2_distributed_amd runs only on the MI355X HIP path: move the inputs to a cuda "
+                               "device (there is no CPU fallback)")
+        return eng.backbone_forward(idx)
 
 
 class GPT2(nn.Module):
@@ -150,7 +185,26 @@ class GPT2(nn.Module):
         self.lm_head.weight = self.transformer.wte.weight
         self._pack_arena()
         self._engine = None
-        self.precision = "auto"  # "auto": follow torch.autocast("cuda"); or force "bf16" / "fp32"
+        self.precision = "auto"
+        self._bind_submodules()
+
+    def _bind_submodules(self):
+        self.transformer._bind_owner(self, None)
+        for i, blk in enumerate(self.transformer.h):
+            blk._bind_owner(self, i)
+            blk.attn._bind_owner(self, i)
+            blk.mlp._bind_owner(self, i)
+
+    # copies (copy.deepcopy / pickling) get their own engine and re-point their sub-modules at themselves
+    def __getstate__(self):
+        st = self.__dict__.copy()
+        st["_engine"] = None
+        return st
+
+    def __setstate__(self, st):
+        super().__setstate__(st)
+        self._rebind(self._arena)  # a copied Parameter is a clone, no longer a view of the copied arena
+        self._bind_submodules()  # "auto": follow torch.autocast("cuda"); or force "bf16" / "fp32"
 
     # ---- flat arena ------------------------------------------------------------------------------
     def _pack_arena(self):

@@ -6,29 +6,49 @@ Replaces the reference's ``DDP(model, device_ids=[device])`` / ``FSDP(model, ...
 * ``init_distributed()``: same contract as the reference (env:// rendezvous from torchrun,
   ``LOCAL_RANK`` -> device).
 * ``DistributedDataParallel(model)``: broadcasts the flat fp32 arena from rank 0 once (C2) and
-  all-reduces (average) the flat fp32 grad arena in ``bucket_mb`` buckets. Buckets are issued
-  asynchronously from inside the engine's backward, as soon as a contiguous arena range is final
-  (blocks finish last-to-first, wte/wpe at the very end), so RCCL runs on its own stream under the
-  remaining backward kernels (C4). No per-forward buffer broadcast (C3): there is no mask buffer.
-  ``no_sync()`` skips the collective on non-final gradient-accumulation micro-steps.
-* ``ShardedDataParallel(model)`` (the ``--training_mode fsdp`` path): ZeRO-style full sharding of
-  the optimizer over the same arena — grads are reduce-scattered (each rank receives the average of
-  its 1/world slice), AdamW updates only the local slice of master weights and moments, and the
-  updated fp32 slice is all-gathered back (C5). The whole model fits one MI355X (288 GB), so
-  parameters are not freed between layers; sharding buys optimizer-state memory and halves the
-  grad traffic of an all-reduce into RS + AG of the same bytes.
+  averages the flat fp32 grad arena in ``bucket_mb`` buckets (C4). Buckets are issued asynchronously
+  from inside the engine's backward as soon as a contiguous arena range is final (blocks finish
+  last-to-first, the embeddings at the very end), so RCCL runs on its own stream under the remaining
+  backward kernels, and the backward does not return before every bucket is reduced: ``p.grad`` is the
+  global average when ``loss.backward()`` returns, exactly as with torch DDP, so the reference loop's
+  ``clip_grad_norm_`` / ``torch.optim.AdamW`` see final gradients. There is no per-forward buffer
+  broadcast (C3): the build has no mask buffer. ``no_sync()`` skips the collective on non-final
+  gradient-accumulation micro-steps.
+* ``FullyShardedDataParallel(model)`` (``--training_mode fsdp``; ``ShardedDataParallel`` is an alias):
+  the reference's FULL_SHARD wrapping with one unit per ``GPT2Block`` plus the root (C5). Each unit's
+  flat parameter range is sharded 1/world per rank: the fp32 master shard (exposed as the wrapper's
+  single ``flat_param``, like FSDP's FlatParameter with use_orig_params=False), its grad and the AdamW
+  moments live only on the owning rank. In the forward the engine asks for each unit just before it
+  reads it; the wrapper all-gathers that unit in the compute precision (bf16 under autocast, like
+  MixedPrecision(param_dtype=bf16)) and prefetches the NEXT unit's all-gather on RCCL's stream while
+  the current unit computes. In the backward each unit's gradient range is reduce-scattered (bf16
+  under autocast, like reduce_dtype=bf16) the moment the engine marks it final, overlapped with the
+  remaining backward. MI355X-first difference: a gathered unit stays resident until the next optimizer
+  step (288 GB HBM holds every unit of every BASELINE model), so the backward does not re-gather it and
+  gradient-accumulation micro-steps gather once per optimizer step; the math is FULL_SHARD's.
 
-The bucketing logic is engine-agnostic (``BucketedReducer`` takes a flat tensor and ready ranges),
-so it is tested on CPU with gloo.
+Gradient scaling: every collective is a SUM. A synced backward computes its gradients pre-divided by
+world (``GradHooks.begin_backward``); gradients accumulated earlier (no_sync micro-steps, or an
+accumulation without no_sync) are divided once before it. SUM then yields the average on any backend,
+so the gloo-tested path is the RCCL path.
+
+The bucketing / shard planning is engine-agnostic (``BucketedReducer``, ``plan_shards``), so it is
+tested on CPU with gloo.
 """
 from __future__ import annotations
 
 import contextlib
 import os
+from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
+import torch.nn as nn
+
+from .engine import GradHooks
+
+SHARD_ALIGN = 64  # elements: 256-B aligned shard chunks (16-B vector kernels, RCCL chunking)
 
 
 def local_device_index() -> int:
@@ -54,25 +74,40 @@ def is_primary() -> bool:
     return dist.get_rank() == 0 if dist.is_initialized() else True
 
 
+def unit_ranges(layout, n_layer: int) -> List[Tuple[str, int, int]]:
+    """The FSDP units / DDP ready ranges of the arena, in arena order: "embed" (wte, wpe), "h.<l>" (one
+    GPT2Block each: transformer_auto_wrap_policy({GPT2Block}), train_gpt2_distributed.py:146-161) and
+    "head" (ln_f). The root unit of the reference is embed + head (two arena ranges)."""
+    starts = {n: s.offset for n, s in layout.slots.items()}
+    out = [("embed", 0, starts["transformer.h.0.ln1.weight"])]
+    for l in range(n_layer):
+        lo = starts[f"transformer.h.{l}.ln1.weight"]
+        hi = starts[f"transformer.h.{l+1}.ln1.weight"] if l + 1 < n_layer else starts["transformer.ln_f.weight"]
+        out.append((f"h.{l}", lo, hi))
+    out.append(("head", starts["transformer.ln_f.weight"], layout.total))
+    return out
+
+
+def backward_order(units):
+    """The order the engine marks ranges final: head, h.L-1 .. h.0, embed."""
+    return [units[-1]] + list(reversed(units[1:-1])) + [units[0]]
+
+
 class BucketedReducer:
-    """Averages a flat gradient tensor across the group in contiguous buckets.
+    """SUM-all-reduces a flat gradient tensor across the group in contiguous buckets.
 
     ``order`` lists (name, lo, hi) ranges of ``flat`` in the order they become final during backward.
     ``mark_ready(name)`` is called when a range is final; once the ready-but-unsent span reaches
-    ``bucket_bytes`` (or at ``flush``) an async all-reduce of that span is issued. Ranges must become
-    ready so that the unsent span stays contiguous (true for reverse arena order)."""
+    ``bucket_bytes`` an async all-reduce of that span is issued. ``finish()`` issues the tail and makes
+    the caller's stream wait for every bucket. Ranges must become ready so that the unsent span stays
+    contiguous (true for reverse arena order)."""
 
-    def __init__(self, flat: torch.Tensor, order: List[Tuple[str, int, int]], bucket_mb: float = 64.0,
-                 group=None, mode: str = "allreduce"):
+    def __init__(self, flat: torch.Tensor, order: List[Tuple[str, int, int]], bucket_mb: float = 64.0, group=None):
         self.flat = flat
         self.order = order
         self.index = {n: i for i, (n, _, _) in enumerate(order)}
-        self.bucket_elems = int(bucket_mb * 1024 * 1024 / flat.element_size())
+        self.bucket_elems = max(1, int(bucket_mb * 1024 * 1024 / flat.element_size()))
         self.group = group
-        self.world = dist.get_world_size(group)
-        self.rank = dist.get_rank(group)
-        self.mode = mode
-        self.use_avg = dist.get_backend(group) == "nccl"
         self.reset()
 
     def reset(self):
@@ -80,7 +115,7 @@ class BucketedReducer:
         self.pending_lo = None  # unsent contiguous span [lo, hi)
         self.pending_hi = None
         self.works = []
-        self.post = []          # gloo: spans to rescale after wait
+        self.launched = 0       # buckets issued during the backward (before finish)
 
     def mark_ready(self, name: str):
         i = self.index[name]
@@ -91,8 +126,10 @@ class BucketedReducer:
             if self.pending_lo is None:
                 self.pending_lo, self.pending_hi = lo, hi
             else:
-                # ranges arrive in descending arena order
-                assert hi <= self.pending_lo + 0 or lo >= self.pending_hi, "non-contiguous ready order"
+                if not (hi <= self.pending_lo or lo >= self.pending_hi):
+                    raise RuntimeError("BucketedReducer: overlapping ready ranges")
+                if hi != self.pending_lo and lo != self.pending_hi:
+                    raise RuntimeError("BucketedReducer: non-contiguous ready order")
                 self.pending_lo = min(self.pending_lo, lo)
                 self.pending_hi = max(self.pending_hi, hi)
             self.next += 1
@@ -103,28 +140,53 @@ class BucketedReducer:
         if self.pending_lo is None:
             return
         span = self.flat[self.pending_lo:self.pending_hi]
-        if self.use_avg:
-            w = dist.all_reduce(span, op=dist.ReduceOp.AVG, group=self.group, async_op=True)
-        else:
-            w = dist.all_reduce(span, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-            self.post.append(span)
-        self.works.append(w)
+        self.works.append(dist.all_reduce(span, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+        self.launched += 1
         self.pending_lo = self.pending_hi = None
 
-    def flush(self):
-        """Mark everything ready, launch the tail and wait (current stream waits on RCCL)."""
+    def finish(self):
+        """Issue whatever is left, then make the current stream wait on every bucket (nccl: a stream
+        wait, the host does not block; gloo: the host waits)."""
         if self.next < len(self.order):
             self.mark_ready(self.order[-1][0])
         self._launch()
         for w in self.works:
             w.wait()
-        for span in self.post:
-            span.mul_(1.0 / self.world)
-        self.works, self.post = [], []
         self.reset()
 
 
-class DistributedDataParallel(torch.nn.Module):
+class _DPHooks(GradHooks):
+    """The gradient side shared by DDP and FSDP: 1/world pre-scaling and the no_sync switch."""
+
+    def __init__(self, engine, world: int):
+        self.engine = engine
+        self.world = world
+        self.sync = True
+
+    def begin_backward(self) -> float:
+        if not self.sync or self.world == 1:
+            return 1.0
+        if self.engine.grad_dirty:  # gradients accumulated before this synced backward: divide them too
+            from . import _lib as K
+            K.scale_(self.engine.grad, 1.0 / self.world)
+        return 1.0 / self.world
+
+
+class _DDPHooks(_DPHooks):
+    def __init__(self, engine, world, reducer):
+        super().__init__(engine, world)
+        self.reducer = reducer
+
+    def ready(self, name):
+        if self.sync and self.world > 1:
+            self.reducer.mark_ready(name)
+
+    def end_backward(self):
+        if self.sync and self.world > 1:
+            self.reducer.finish()
+
+
+class DistributedDataParallel(nn.Module):
     """DDP for the arena model: same call surface as torch DDP for the reference loop."""
 
     def __init__(self, module, device_ids=None, bucket_mb: float = 64.0, broadcast: bool = True):
@@ -132,132 +194,305 @@ class DistributedDataParallel(torch.nn.Module):
         self.module = module
         eng = module.engine()
         self.engine = eng
-        if broadcast and dist.get_world_size() > 1:
+        world = dist.get_world_size()
+        if broadcast and world > 1:
             dist.broadcast(module.arena, src=0)
             eng.refresh_shadow()
-        # ready order = reverse arena order; one range per engine "ready" event
-        self.reducer = BucketedReducer(eng.grad, self._ready_ranges(module), bucket_mb)
-        self._sync = True
-        eng.grad_sync = self._on_event
-
-    @staticmethod
-    def _ready_ranges(module):
-        lay = module.layout
-        L = module.config.n_layer
-        total = lay.total
-        starts = {n: s.offset for n, s in lay.slots.items()}
-        order = []
-        lnf_lo = starts["transformer.ln_f.weight"]
-        order.append(("transformer.ln_f.bias", lnf_lo, total))
-        hi = lnf_lo
-        for l in reversed(range(L)):
-            lo = starts[f"transformer.h.{l}.ln1.weight"]
-            order.append((f"transformer.h.{l}.ln1.weight", lo, hi))
-            hi = lo
-        order.append(("transformer.wte.weight", 0, hi))
-        return order
-
-    def _on_event(self, event, name=None):
-        if event == "ready" and self._sync:
-            self.reducer.mark_ready(name)
+        units = unit_ranges(module.layout, module.config.n_layer)
+        self.reducer = BucketedReducer(eng.grad, backward_order(units), bucket_mb)
+        self.hooks = _DDPHooks(eng, world, self.reducer)
+        eng.grad_sync = self.hooks
 
     @contextlib.contextmanager
     def no_sync(self):
-        old = self._sync
-        self._sync = False
+        old = self.hooks.sync
+        self.hooks.sync = False
         try:
             yield
         finally:
-            self._sync = old
+            self.hooks.sync = old
 
     def forward(self, *args, **kwargs):
         return self.module(*args, **kwargs)
 
     def finish_gradient_sync(self):
-        """Wait for every bucket (called by the optimizer step wrapper / trainer)."""
-        if self._sync:
-            self.reducer.flush()
+        """Kept for callers of round 1: the backward itself completes the gradient collective."""
 
     def configure_optimizers(self, *a, **kw):
-        opt = self.module.configure_optimizers(*a, **kw)
-        return _SyncedOptimizer(opt, self)
+        return self.module.configure_optimizers(*a, **kw)
 
     def state_dict(self, *a, **kw):
         return self.module.state_dict(*a, **kw)
 
 
-class _SyncedOptimizer:
-    """Optimizer proxy: step() first completes the gradient collective."""
+# --------------------------------------------------------------------------------------------------
+# FSDP
+# --------------------------------------------------------------------------------------------------
+@dataclass
+class ShardPlan:
+    name: str
+    lo: int          # arena range of the unit
+    hi: int
+    per: int         # elements per rank (padded)
+    soff: int        # offset of this unit's chunk in every rank's shard arena
 
-    def __init__(self, opt, ddp):
-        self.opt = opt
-        self.ddp = ddp
-
-    def step(self, closure=None):
-        self.ddp.finish_gradient_sync()
-        return self.opt.step(closure)
-
-    def zero_grad(self, set_to_none=True):
-        self.opt.zero_grad(set_to_none)
-
-    def __getattr__(self, k):
-        return getattr(self.opt, k)
+    @property
+    def n(self):
+        return self.hi - self.lo
 
 
-class ShardedDataParallel(DistributedDataParallel):
-    """ZeRO-style sharded optimizer over the arena (the build's --training_mode fsdp)."""
+def plan_shards(units, world: int, align: int = SHARD_ALIGN) -> Tuple[List[ShardPlan], int]:
+    """Every unit's range split into `world` equal chunks of `per` elements (rank r owns unit elements
+    [r*per, (r+1)*per), zero-padded past the unit's end); any world size (3, 6, 12 ...) works."""
+    plans, off = [], 0
+    for name, lo, hi in units:
+        per = -(-(hi - lo) // world)
+        per = -(-per // align) * align
+        plans.append(ShardPlan(name, lo, hi, per, off))
+        off += per
+    return plans, off
 
-    def __init__(self, module, device_ids=None, bucket_mb: float = 64.0):
-        super().__init__(module, device_ids, bucket_mb)
-        W = dist.get_world_size()
-        total = module.layout.total
-        per = (total + W - 1) // W
-        per = (per + 63) // 64 * 64
-        self.per = per
-        self.padded = per * W
-        r = dist.get_rank()
-        self.lo, self.hi = min(r * per, total), min((r + 1) * per, total)
-        self.engine.grad_sync = None  # reduce-scatter happens at the end (one fused collective)
+
+class _FSDPHooks(_DPHooks):
+    def __init__(self, fsdp, world):
+        super().__init__(fsdp.engine, world)
+        self.fsdp = fsdp
+
+    def ready(self, name):
+        if self.sync:
+            self.fsdp._reduce_scatter(name)
+
+    def end_backward(self):
+        if self.sync:
+            self.fsdp._finish_reduce()
+
+    def fwd_unit(self, unit):
+        self.fsdp._gather_for(unit)
+
+
+class FullyShardedDataParallel(nn.Module):
+    """FULL_SHARD data parallelism over per-GPT2Block units (see the module docstring)."""
+
+    def __init__(self, module, device_ids=None, bucket_mb: float = 64.0, prefetch: bool = True):
+        super().__init__()
+        self.module = module
+        eng = module.engine()
+        self.engine = eng
+        self.world = dist.get_world_size()
+        self.rank = dist.get_rank()
+        self.prefetch = prefetch
+        W, r = self.world, self.rank
+        if W > 1:
+            dist.broadcast(module.arena, src=0)
+        self.units = unit_ranges(module.layout, module.config.n_layer)
+        self.plans, self.shard_total = plan_shards(self.units, W)
+        self.plan = {p.name: p for p in self.plans}
+        self.order = [p.name for p in self.plans]  # forward order = arena order
+        dev = module.arena.device
+        master = torch.zeros(self.shard_total, dtype=torch.float32, device=dev)
+        for p in self.plans:  # this rank's chunk of every unit
+            a, b = p.lo + r * p.per, min(p.hi, p.lo + (r + 1) * p.per)
+            if b > a:
+                master[p.soff:p.soff + b - a].copy_(module.arena[a:b])
+        # FSDP's FlatParameter (use_orig_params=False): the only parameter the wrapper exposes
+        self.flat_param = nn.Parameter(master)
+        self.grad_shard = torch.zeros_like(master)
+        self.shard_bf16 = torch.empty(self.shard_total, dtype=torch.bfloat16, device=dev)
+        self._bufs: Dict[tuple, torch.Tensor] = {}
+        self._valid: Dict[str, Optional[torch.dtype]] = {u: None for u in self.order}
+        self._pending: Dict[str, tuple] = {}       # unit -> (work, dtype) of an in-flight all-gather
+        self._rs_works: List[tuple] = []            # (unit, work, out) of in-flight reduce-scatters
+        self._bf16_fresh = False                     # shard_bf16 == bf16(flat_param) (set by our AdamW)
+        self._seen_version = None
+        self.hooks = _FSDPHooks(self, W)
+        eng.grad_sync = self.hooks
+        eng.param_provider = self.hooks
+        eng.zero_grad()
+        eng.bind_grads()
+
+    # ---- parameters: the flat shard only (torch optimizers / clip_grad_norm_ see what FSDP exposes) ----
+    def parameters(self, recurse: bool = True):
+        yield self.flat_param
+
+    def named_parameters(self, prefix: str = "", recurse: bool = True, remove_duplicate: bool = True):
+        yield (prefix + ("." if prefix else "") + "flat_param", self.flat_param)
+
+    def memory_report(self) -> dict:
+        """Bytes per rank: sharded state (fp32 master, grad, AdamW moments, bf16 AG source) vs the
+        resident compute views (fp32 params, bf16 shadow + transposed shadow, transient fp32 grad arena,
+        collective staging). DDP keeps every one of the sharded tensors whole."""
+        n_full = self.module.arena.numel()
+        sharded = self.shard_total * (4 + 4 + 8 + 2)
+        views = n_full * (4 + 2 + 2 + 4)
+        staging = sum(t.numel() * t.element_size() for t in self._bufs.values())
+        return {"params": n_full, "world": self.world, "sharded_state_bytes": sharded,
+                "ddp_equivalent_state_bytes": n_full * (4 + 4 + 8),
+                "compute_view_bytes": views, "staging_bytes": staging}
+
+    # ---- buffers ------------------------------------------------------------------------------------
+    def _buf(self, kind, unit, dtype, n):
+        key = (kind, unit, dtype)
+        t = self._bufs.get(key)
+        if t is None:
+            t = torch.empty(n, dtype=dtype, device=self.flat_param.device)
+            self._bufs[key] = t
+        return t
+
+    # ---- forward: per-unit all-gather with prefetch ---------------------------------------------------
+    def mark_params_updated(self, bf16_fresh: bool):
+        """Called after an optimizer step on flat_param (our AdamW also wrote shard_bf16)."""
+        self._valid = {u: None for u in self.order}
+        self._bf16_fresh = bf16_fresh
+        self._seen_version = self.flat_param._version
+
+    def _check_version(self):
+        if self._seen_version is None or self.flat_param._version != self._seen_version:
+            # a step we did not see (torch optimizer, load): every gathered unit is stale
+            self._valid = {u: None for u in self.order}
+            self._bf16_fresh = False
+            self._seen_version = self.flat_param._version
+
+    def _issue_gather(self, unit, dtype):
+        from . import _lib as K
+        p = self.plan[unit]
+        if dtype == torch.bfloat16:
+            if not self._bf16_fresh:
+                K.cast_f32_bf16(self.flat_param.detach(), self.shard_bf16, self.shard_total)
+                self._bf16_fresh = True
+            src = self.shard_bf16[p.soff:p.soff + p.per]
+        else:
+            src = self.flat_param.detach()[p.soff:p.soff + p.per]
+        out = self._buf("ag", unit, dtype, p.per * self.world)
+        if self.world == 1:
+            out.copy_(src)
+            work = None
+        else:
+            work = dist.all_gather_into_tensor(out, src, async_op=True)
+        self._pending[unit] = (work, dtype)
+
+    def _gather_for(self, unit):
+        from . import _lib as K
+        eng = self.engine
+        dtype = eng.compute_dtype()
+        self._check_version()
+        if self._valid.get(unit) != dtype:
+            if unit not in self._pending or self._pending[unit][1] != dtype:
+                self._issue_gather(unit, dtype)
+        if self.prefetch:  # the next unit's all-gather rides under this unit's compute
+            i = self.order.index(unit)
+            if i + 1 < len(self.order):
+                nxt = self.order[i + 1]
+                if self._valid.get(nxt) != dtype and nxt not in self._pending:
+                    self._issue_gather(nxt, dtype)
+        if self._valid.get(unit) == dtype:
+            return
+        work, _ = self._pending.pop(unit)
+        if work is not None:
+            work.wait()
+        p = self.plan[unit]
+        out = self._buf("ag", unit, dtype, p.per * self.world)
+        bf = eng.shadow[p.lo:p.hi] if dtype == torch.bfloat16 else None
+        K.fsdp_unpack(out, self.module.arena[p.lo:p.hi], bf, p.n)
+        if dtype == torch.bfloat16:
+            names = [n for n, s in self.module.layout.slots.items() if p.lo <= s.offset < p.hi]
+            eng.refresh_shadowT(names)
+        self._valid[unit] = dtype
+
+    # ---- backward: per-unit reduce-scatter as ranges become final ----------------------------------------
+    def _reduce_scatter(self, unit):
+        from . import _lib as K
+        p = self.plan[unit]
+        eng = self.engine
+        dtype = eng.bwd_act  # reduce_dtype = the compute precision (bf16 under autocast)
+        inp = self._buf("rs_in", unit, dtype, p.per * self.world)
+        K.fsdp_pack(eng.grad[p.lo:p.hi], inp, p.n, p.per * self.world)
+        out = self._buf("rs_out", unit, dtype, p.per)
+        if self.world == 1:
+            out.copy_(inp)
+            work = None
+        else:
+            work = dist.reduce_scatter_tensor(out, inp, op=dist.ReduceOp.SUM, async_op=True)
+        self._rs_works.append((unit, work, out))
+
+    def _finish_reduce(self):
+        from . import _lib as K
+        done = {u for u, _, _ in self._rs_works}
+        for u in self.order:  # ranges the engine did not mark (e.g. a sub-module backward): reduce them too
+            if u not in done:
+                self._reduce_scatter(u)
+        # the packed inputs hold this backward's gradients: the full arena restarts from zero
+        K.zero_(self.engine.grad)
+        self.engine.grad_dirty = False
+        for u, work, out in self._rs_works:
+            if work is not None:
+                work.wait()
+            p = self.plan[u]
+            K.fsdp_accum(out, self.grad_shard[p.soff:p.soff + p.per], p.per, accumulate=True)
+        self._rs_works = []
+        self.flat_param.grad = self.grad_shard
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        old = self.hooks.sync
+        self.hooks.sync = False
+        try:
+            yield
+        finally:
+            self.hooks.sync = old
+
+    def forward(self, *args, **kwargs):
+        return self.module(*args, **kwargs)
 
     def finish_gradient_sync(self):
-        eng = self.engine
-        W = dist.get_world_size()
-        g = eng.grad
-        if g.numel() < self.padded:
-            raise RuntimeError("arena must be padded to the shard grid")
-        inp = g[:self.padded]
-        shard = torch.empty(self.per, dtype=g.dtype, device=g.device)
-        op = dist.ReduceOp.AVG if dist.get_backend() == "nccl" else dist.ReduceOp.SUM
-        dist.reduce_scatter_tensor(shard, inp, op=op)
-        if op == dist.ReduceOp.SUM:
-            shard.mul_(1.0 / W)
-        g[self.lo:self.hi].copy_(shard[:self.hi - self.lo])
+        """Kept for callers of round 1: the backward itself completes the gradient collective."""
+
+    def zero_grad(self, set_to_none: bool = True):
+        from . import _lib as K
+        K.zero_(self.grad_shard)
+        self.flat_param.grad = None if set_to_none else self.grad_shard
+        self.engine.zero_grad()
 
     def configure_optimizers(self, weight_decay=0.1, learning_rate=1e-4, betas=(0.9, 0.95), device_type=None,
                              eps=1e-8):
-        from .optim import FusedAdamW
-        opt = FusedAdamW(self.module, lr=learning_rate, betas=betas, eps=eps, weight_decay=weight_decay,
-                         shard=(self.lo, self.hi))
-        return _ShardedOptimizer(opt, self)
+        from .optim import ShardedAdamW
+        return ShardedAdamW(self, lr=learning_rate, betas=betas, eps=eps, weight_decay=weight_decay)
+
+    # ---- full state (checkpointing): collective, every rank calls --------------------------------------
+    @torch.no_grad()
+    def full_arena(self) -> torch.Tensor:
+        """The fp32 master parameters of every unit, all-gathered (FULL_STATE_DICT; fixes the reference's
+        rank-0-only early return before this collective, train_gpt2_distributed.py:81-94)."""
+        arena = torch.zeros_like(self.module.arena)
+        for p in self.plans:
+            src = self.flat_param.detach()[p.soff:p.soff + p.per]
+            out = torch.empty(p.per * self.world, dtype=torch.float32, device=arena.device)
+            if self.world == 1:
+                out.copy_(src)
+            else:
+                dist.all_gather_into_tensor(out, src)
+            arena[p.lo:p.hi].copy_(out[:p.n])
+        return arena
+
+    def state_dict(self, *a, **kw):
+        arena = self.full_arena()
+        lay = self.module.layout
+        return {n: lay.view(arena, n).clone() for n in self.module.state_dict()
+                if n in lay.slots} | ({"lm_head.weight": lay.view(arena, "transformer.wte.weight").clone()}
+                                      if "lm_head.weight" in self.module.state_dict() else {})
+
+    @torch.no_grad()
+    def load_full_state_dict(self, sd):
+        m = self.module
+        for n, p in m.named_parameters():
+            p.copy_(sd[n])
+        for pl in self.plans:
+            a, b = pl.lo + self.rank * pl.per, min(pl.hi, pl.lo + (self.rank + 1) * pl.per)
+            chunk = self.flat_param.detach()[pl.soff:pl.soff + pl.per]
+            chunk.zero_()
+            if b > a:
+                chunk[:b - a].copy_(m.arena[a:b])
+        self.mark_params_updated(False)
+        self._seen_version = None  # force a refresh at the next forward
 
 
-class _ShardedOptimizer(_SyncedOptimizer):
-    def step(self, closure=None):
-        self.ddp.finish_gradient_sync()
-        out = self.opt.step(closure)
-        # the kernel's norm covers this rank's slice: the clip_grad_norm_ value is the global one
-        # (train_gpt2_distributed.py:419-421 on the full grads)
-        n2 = self.opt.grad_norm.square()
-        dist.all_reduce(n2)
-        self.opt.grad_norm.copy_(n2.sqrt())
-        # all-gather the updated fp32 master slices, then refresh the bf16 shadow once
-        m = self.ddp.module
-        arena = m.arena
-        shard = torch.zeros(self.ddp.per, dtype=arena.dtype, device=arena.device)
-        n = self.ddp.hi - self.ddp.lo
-        shard[:n].copy_(arena[self.ddp.lo:self.ddp.hi])
-        full = torch.empty(self.ddp.padded, dtype=arena.dtype, device=arena.device)
-        dist.all_gather_into_tensor(full, shard)
-        arena.copy_(full[:arena.numel()])
-        m.engine().refresh_shadow()
-        return out
+ShardedDataParallel = FullyShardedDataParallel

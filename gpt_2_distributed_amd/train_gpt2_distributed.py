@@ -13,8 +13,8 @@ checkpoints every --save_every optimizer steps between barriers. Differences, al
   * DDP syncs gradients only on the last micro-step (``no_sync`` elsewhere; same math);
   * logged tok/s is the whole-node SUM and MFU is reported (the reference averages per-GPU tok/s,
     stats_tracker.py:25-34); host syncs happen only on log steps;
-  * checkpoints are collective-correct under fsdp, and --resume restores model + optimizer
-    (the reference's load_checkpoint is a stub, :104-111).
+  * checkpoints are collective-correct under fsdp, and --resume restores model + optimizer + the
+    dropout stream + the data position (the reference's load_checkpoint is a stub, :104-111).
 """
 from __future__ import annotations
 
@@ -31,7 +31,7 @@ import torch.distributed as dist
 
 from . import dataloader as gpt2_dataloader
 from .model import GPT2, GPT2Config, MODEL_SIZES
-from .parallel import DistributedDataParallel, ShardedDataParallel, init_distributed, is_primary
+from .parallel import DistributedDataParallel, FullyShardedDataParallel, init_distributed, is_primary
 
 SEED = 42
 PEAK_BF16 = 2.5166e15
@@ -62,16 +62,22 @@ def build_parser():
     return p
 
 
-def save_checkpoint(model, opt, step: int, out_dir: str):
+def save_checkpoint(model, opt, step: int, out_dir: str, trainer_state: dict = None):
     """step_{:07d}/model.pt (reference state_dict keys) + optim.pt (train_gpt2_distributed.py:67-101).
-    Collective-correct: under fsdp every rank writes its optimizer shard (optim_rank{r}.pt)."""
+    Collective-correct (the reference returns early on non-primary ranks before FSDP's full-state
+    all-gather, :81-94): under fsdp every rank joins the parameter gather and writes its optimizer shard
+    (optim_rank{r}.pt). trainer.json keeps what an exact resume needs beyond the weights: the dropout
+    stream position and the epoch / micro-batch the next step starts from."""
     base = model.module if hasattr(model, "module") else model
     out = os.path.join(out_dir, f"step_{step:07d}")
-    sharded = isinstance(model, ShardedDataParallel)
+    sharded = isinstance(model, FullyShardedDataParallel)
+    sd = model.state_dict() if sharded else base.state_dict()  # fsdp: a collective on every rank
     if is_primary():
         os.makedirs(out, exist_ok=True)
-        sd = {k: v.detach().cpu() for k, v in base.state_dict().items()}
-        torch.save(sd, os.path.join(out, "model.pt"))
+        torch.save({k: v.detach().cpu() for k, v in sd.items()}, os.path.join(out, "model.pt"))
+        st = dict(trainer_state or {}, step=step, step_seed=base.engine()._step_seed)
+        with open(os.path.join(out, "trainer.json"), "w") as f:
+            json.dump(st, f)
     if dist.is_initialized():
         dist.barrier()
     osd = opt.state_dict()
@@ -86,16 +92,27 @@ def save_checkpoint(model, opt, step: int, out_dir: str):
 
 
 def load_checkpoint(model, opt, ckpt_dir: str):
+    """Restore what save_checkpoint wrote (the reference's load_checkpoint is a stub, :104-111).
+    Returns the trainer state (step, step_seed, epoch, micro)."""
     base = model.module if hasattr(model, "module") else model
     sd = torch.load(os.path.join(ckpt_dir, "model.pt"), map_location="cpu", weights_only=True)
-    with torch.no_grad():
-        for n, p in base.named_parameters():
-            p.copy_(sd[n])
-    base.engine().refresh_shadow()
-    name = f"optim_rank{dist.get_rank()}.pt" if isinstance(model, ShardedDataParallel) else "optim.pt"
+    if isinstance(model, FullyShardedDataParallel):
+        model.load_full_state_dict(sd)
+    else:
+        with torch.no_grad():
+            for n, p in base.named_parameters():
+                p.copy_(sd[n])
+        base.engine().refresh_shadow()
+    name = f"optim_rank{dist.get_rank()}.pt" if isinstance(model, FullyShardedDataParallel) else "optim.pt"
     osd = torch.load(os.path.join(ckpt_dir, name), map_location="cpu", weights_only=True)
     opt.load_state_dict(osd)
-    return int(osd["step"])
+    st = {"step": int(osd["step"])}
+    tpath = os.path.join(ckpt_dir, "trainer.json")
+    if os.path.exists(tpath):
+        with open(tpath) as f:
+            st.update(json.load(f))
+        base.engine()._step_seed = int(st.get("step_seed", 0))
+    return st
 
 
 def main(argv=None):
@@ -140,36 +157,43 @@ def main(argv=None):
     if args.training_mode == "ddp":
         model = DistributedDataParallel(base)
     elif args.training_mode == "fsdp":
-        model = ShardedDataParallel(base)
+        model = FullyShardedDataParallel(base)
     else:
         model = base
     optim = model.configure_optimizers(weight_decay=0.1, learning_rate=args.lr, betas=(0.9, 0.95))
-    global_step = 0
+    global_step, start_epoch, skip = 0, 0, 0
     if args.resume:
-        global_step = load_checkpoint(model, optim, args.resume)
+        st = load_checkpoint(model, optim, args.resume)
+        global_step = st["step"]
+        start_epoch, skip = int(st.get("epoch", 0)), int(st.get("micro", 0))
     fpt = 6 * (config.n_layer * 12 * config.n_embd ** 2 + config.vocab_size * config.n_embd) + \
         12 * config.n_layer * args.seq_len * config.n_embd
     optim.zero_grad()
     tok_per_step = args.batch * args.grad_accum_steps * args.seq_len * world
     t_last, steps_since = time.perf_counter(), 0
-    for epoch in range(args.epochs):
+    done, epoch, micro = False, start_epoch, 0
+    for epoch in range(start_epoch, args.epochs):
         ds.set_epoch(epoch)  # as the reference; persistent workers keep epoch 0
         if is_primary():
             print(f"\n==== Epoch {epoch} ====")
         batches = dl if dl is not None else gpt2_dataloader.iter_batches(paths, args.seq_len, args.batch, 1,
                                                                        epoch=epoch)
-        accum = 0
+        micro = 0
         for x, y in batches:
+            if skip:  # resume: the micro-batches the checkpointed steps already consumed
+                skip -= 1
+                micro += 1
+                continue
             x = x.to(device, non_blocking=True)
             y = y.to(device, non_blocking=True)
-            last = (accum + 1) % args.grad_accum_steps == 0
+            last = (micro + 1) % args.grad_accum_steps == 0
             ctx = model.no_sync() if (hasattr(model, "no_sync") and not last) else _Null()
             with ctx:
                 with torch.autocast("cuda", dtype=torch.bfloat16):  # as train_gpt2_distributed.py:404
                     _, loss = model(x, labels=y)
                     loss = loss / args.grad_accum_steps
                 loss.backward()
-            accum += 1
+            micro += 1
             if not last:
                 continue
             optim.step()
@@ -187,12 +211,14 @@ def main(argv=None):
                                       "mfu": round(tps * fpt / (world * PEAK_BF16), 4)}), flush=True)
                 t_last, steps_since = now, 0
             if global_step % args.save_every == 0:
-                save_checkpoint(model, optim, global_step, args.save_dir)
+                save_checkpoint(model, optim, global_step, args.save_dir, {"epoch": epoch, "micro": micro})
             if args.max_steps and global_step >= args.max_steps:
+                done = True
                 break
-        if args.max_steps and global_step >= args.max_steps:
+        if done:
             break
-    save_checkpoint(model, optim, global_step, args.save_dir)
+    pos = {"epoch": epoch, "micro": micro} if done else {"epoch": args.epochs, "micro": 0}
+    save_checkpoint(model, optim, global_step, args.save_dir, pos)
     if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()

@@ -26,17 +26,20 @@
 extern "C" {
 #endif
 
-#define GPT2MI_ABI_VERSION 4
+#define GPT2MI_ABI_VERSION 5
 
 const char* gpt2mi_last_error(void);
 int gpt2mi_abi_version(void); /* returns GPT2MI_ABI_VERSION of the built library */
 
-/* K1: x[b,t,:] = drop(wte[idx[b,t],:] + wpe[t,:])  — model.py:295-304 (embedding, add, dropout). */
-int gpt2mi_embed_fwd(const int64_t* idx, const float* wte, const float* wpe, float* x, int B, int T, int C,
-                     float p, uint64_t seed, void* stream);
-/* embedding_dense_backward of both tables: dwte[idx] += g, dwpe[t] += sum_b g (g = dres masked). */
-int gpt2mi_embed_bwd(const int64_t* idx, const float* dres, float* dwte, float* dwpe, int B, int T, int C,
-                     float p, uint64_t seed, void* stream);
+/* K1: x[b,t,:] = drop(wte[idx[b,t],:] + wpe[t,:])  — model.py:295-304 (embedding, add, dropout).
+ * Rows with t >= T_valid are sequence padding (T rounded up to the attention tile by the engine): x = 0
+ * there and neither table is read (wpe may have only T_valid rows). */
+int gpt2mi_embed_fwd(const int64_t* idx, const float* wte, const float* wpe, float* x, int B, int T, int T_valid,
+                     int C, float p, uint64_t seed, void* stream);
+/* embedding_dense_backward of both tables: dwte[idx] += g, dwpe[t] += sum_b g (g = dres masked); rows
+ * t >= T_valid are skipped. */
+int gpt2mi_embed_bwd(const int64_t* idx, const float* dres, float* dwte, float* dwpe, int B, int T, int T_valid,
+                     int C, float p, uint64_t seed, void* stream);
 
 /* K2: nn.LayerNorm forward — model.py:204,210,247 (used :215,218,311). y_bf16 and/or y_f32 may be NULL. */
 int gpt2mi_layernorm_fwd(const float* x, const float* w, const float* b, uint16_t* y_bf16, float* y_f32,
@@ -89,7 +92,8 @@ int gpt2mi_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* do
 
 /* K13: F.cross_entropy(logits.view(-1,V), labels.view(-1), ignore_index) — model.py:357-359.
  * logits bf16 [M, ld]; writes loss_rows [M], lse [M], loss[0] = mean, inv_count[0] = 1/#valid and, if
- * dlogits != NULL, dlogits = softmax - onehot (bf16 [M, ldd], unscaled, zero in columns >= V). */
+ * dlogits != NULL, dlogits = softmax - onehot (bf16 [M, ldd], unscaled, zero in columns >= V). A label
+ * outside [0, V) other than ignore_index (F.cross_entropy raises) makes its loss row and dlogits row NaN. */
 int gpt2mi_xent_fwd(const uint16_t* logits, int ld, const int64_t* labels, float* loss_rows, float* lse,
                     uint16_t* dlogits, int ldd, int M, int V, int ignore_index, float* loss, float* inv_count,
                     void* stream);
@@ -142,6 +146,33 @@ int gpt2mi_transpose_bf16(const uint16_t* src, uint16_t* dst, int R, int C, int 
 int gpt2mi_transpose_bf16_batched(const uint16_t* src, uint16_t* dst, const int64_t* desc, int n,
                                   int64_t total_tiles, void* stream);
 int gpt2mi_cast_f32_bf16(const float* x, uint16_t* y, size_t n, void* stream);
+int gpt2mi_cast_bf16_f32(const uint16_t* x, float* y, size_t n, void* stream);
+
+/* ---- v5: the boundary around the fused step (aux_ops.hip) ---- */
+/* Gradient entering through the returned logits (model.py:351: logits are returned and differentiable):
+ * dl[b*Tp+t][n] = (init ? 0 : alpha_dev[0]*dl) + g[b*Tv+t][n] for t < Tv, n < V; dl columns [V, ldd) = 0;
+ * rows t >= Tv (sequence padding) are zeroed when init, else untouched. dl is the lm_head backward's
+ * dlogits (bf16 [B*Tp, ldd]); g the caller's grad of the [B, Tv, V] logits (row stride ldg). */
+int gpt2mi_dlogits_accum(uint16_t* dl, int ldd, const uint16_t* g, int ldg, int B, int Tp, int Tv, int V,
+                         const float* alpha_dev, int init, void* stream);
+int gpt2mi_dlogits_accum_f32(float* dl, int ldd, const float* g, int ldg, int B, int Tp, int Tv, int V,
+                             const float* alpha_dev, int init, void* stream);
+/* Residual-branch output gradient of a stand-alone sub-module backward (model.py:158,191: resid_drop /
+ * drop2 then the branch bias): out = dres*keep/(1-p) (bf16 [M,C]; fp32 for _f32), dbias += colsum(out). */
+int gpt2mi_branch_bwd(const float* dres, uint16_t* out, float* dbias, int M, int C, float p, uint64_t seed,
+                      void* stream);
+int gpt2mi_branch_bwd_f32(const float* dres, float* out, float* dbias, int M, int C, float p, uint64_t seed,
+                          void* stream);
+/* x *= s (n % 4 == 0): DDP's division of a gradient bucket by the world size before a SUM all-reduce
+ * (torch/nn/parallel/distributed.py reducer; train_gpt2_distributed.py:163). */
+int gpt2mi_scale_f32(float* x, size_t n, float s, void* stream);
+/* FSDP flat units (train_gpt2_distributed.py:146-161, MixedPrecision(param=bf16, reduce=bf16)):
+ * unpack a gathered unit into the fp32 parameter view and the bf16 GEMM shadow (either may be NULL);
+ * pack a unit's fp32 grads into the zero-padded reduce-scatter input (bf16 or fp32);
+ * accumulate the reduce-scattered shard into the fp32 grad shard (= when accumulate == 0). */
+int gpt2mi_fsdp_unpack(const void* src, int src_f32, float* dst_f32, uint16_t* dst_bf16, size_t n, void* stream);
+int gpt2mi_fsdp_pack(const float* src, void* dst, int dst_f32, size_t n, size_t n_pad, void* stream);
+int gpt2mi_fsdp_accum(const void* src, int src_f32, float* dst, size_t n, int accumulate, void* stream);
 int gpt2mi_scale_mul(const float* a, const float* b, float* out, void* stream);
 int gpt2mi_memset_zero(void* ptr, size_t bytes, void* stream);
 

@@ -161,35 +161,46 @@ def cross_entropy(logits, labels):
     return F.cross_entropy(lg, y, ignore_index=-100)
 
 
-def block_forward(x, p, cfg, mode="fp32", drop=None, layer=0):
-    """GPT2Block.forward (model.py:213-219): x + attn(ln1(x)); x + mlp(ln2(x)). ``drop``: optional
-    table of dropout multipliers keep/(1-p) per site (``dropout_ref.step_masks``); None = dropout 0."""
+def attn_forward(x, p, cfg, mode="fp32", drop=None, layer=0):
+    """CausalMultiHeadSelfAttention.forward (model.py:110-159) on the ln1 output x [B,T,C]:
+    resid_drop(proj(attention(qkv(x)))). ``p`` holds the block's parameters (BLOCK_KEYS names)."""
+    dm = (lambda site: drop[(site, layer)]) if drop is not None else (lambda site: None)
+    B, T, C = x.shape
+    H = cfg.n_head
+    D = C // H
+    qkv = linear(x, p["attn.qkv.weight"], p["attn.qkv.bias"], mode)          # [B,T,3C]
+    qkv = qkv.view(B, T, 3, H, D).transpose(1, 3)                           # model.py:124
+    q, k, v = qkv.unbind(dim=2)                                             # [B,H,T,D]
+    y = causal_attention(q, k, v, mode, dm("attn"))
+    y = y.transpose(1, 2).contiguous().view(B, T, C)                        # model.py:155
+    y = linear(y, p["attn.proj.weight"], p["attn.proj.bias"], mode)
+    m = dm("proj")
+    return y if m is None else y * m                                        # resid_drop (model.py:158)
+
+
+def mlp_forward(x, p, cfg, mode="fp32", drop=None, layer=0):
+    """MLP.forward (model.py:186-192) on the ln2 output x: drop2(fc2(drop1(gelu(fc1(x)))))."""
     dm = (lambda site: drop[(site, layer)]) if drop is not None else (lambda site: None)
 
     def dr(t, site):
         m = dm(site)
         return t if m is None else t * m
-    B, T, C = x.shape
-    H = cfg.n_head
-    D = C // H
-    h = layer_norm(x, p["ln1.weight"], p["ln1.bias"], cfg.layer_norm_eps)
-    qkv = linear(h, p["attn.qkv.weight"], p["attn.qkv.bias"], mode)          # [B,T,3C]
-    qkv = qkv.view(B, T, 3, H, D).transpose(1, 3)                           # model.py:124
-    q, k, v = qkv.unbind(dim=2)                                             # [B,H,T,D]
-    y = causal_attention(q, k, v, mode, dm("attn"))
-    y = y.transpose(1, 2).contiguous().view(B, T, C)                        # model.py:155
-    y = dr(linear(y, p["attn.proj.weight"], p["attn.proj.bias"], mode), "proj")  # resid_drop (model.py:158)
-    x = x + y
-    h = layer_norm(x, p["ln2.weight"], p["ln2.bias"], cfg.layer_norm_eps)
-    u = linear(h, p["mlp.fc1.weight"], p["mlp.fc1.bias"], mode)
+    u = linear(x, p["mlp.fc1.weight"], p["mlp.fc1.bias"], mode)
     a = dr(gelu_tanh(u, mode), "fc1")                                       # drop1 (model.py:188)
-    y = dr(linear(a, p["mlp.fc2.weight"], p["mlp.fc2.bias"], mode), "fc2")  # drop2 (model.py:191)
-    return x + y
+    return dr(linear(a, p["mlp.fc2.weight"], p["mlp.fc2.bias"], mode), "fc2")  # drop2 (model.py:191)
 
 
-def forward(params, cfg, idx, labels=None, mode="fp32", drop=None):
-    """GPT2.forward (model.py:335-361) -> (logits, loss). ``drop``: None = dropout 0 (parity runs), else
-    the per-site multipliers of one step (``dropout_ref.step_masks``)."""
+def block_forward(x, p, cfg, mode="fp32", drop=None, layer=0):
+    """GPT2Block.forward (model.py:213-219): x + attn(ln1(x)); x + mlp(ln2(x)). ``drop``: optional
+    table of dropout multipliers keep/(1-p) per site (``dropout_ref.step_masks``); None = dropout 0."""
+    h = layer_norm(x, p["ln1.weight"], p["ln1.bias"], cfg.layer_norm_eps)
+    x = x + attn_forward(h, p, cfg, mode, drop, layer)
+    h = layer_norm(x, p["ln2.weight"], p["ln2.bias"], cfg.layer_norm_eps)
+    return x + mlp_forward(h, p, cfg, mode, drop, layer)
+
+
+def backbone_forward(params, cfg, idx, mode="fp32", drop=None):
+    """GPT2Backbone.forward (model.py:275-313): embeddings -> blocks -> ln_f (fp32 output)."""
     B, T = idx.shape
     if T > cfg.n_positions:
         raise ValueError(f"Sequence length {T} > model max {cfg.n_positions}")
@@ -200,7 +211,13 @@ def forward(params, cfg, idx, labels=None, mode="fp32", drop=None):
         pre = f"transformer.h.{i}."
         p = {k: params[pre + k] for k in BLOCK_KEYS}
         x = block_forward(x, p, cfg, mode, drop, i)
-    x = layer_norm(x, params["transformer.ln_f.weight"], params["transformer.ln_f.bias"], cfg.layer_norm_eps)
+    return layer_norm(x, params["transformer.ln_f.weight"], params["transformer.ln_f.bias"], cfg.layer_norm_eps)
+
+
+def forward(params, cfg, idx, labels=None, mode="fp32", drop=None):
+    """GPT2.forward (model.py:335-361) -> (logits, loss). ``drop``: None = dropout 0 (parity runs), else
+    the per-site multipliers of one step (``dropout_ref.step_masks``)."""
+    x = backbone_forward(params, cfg, idx, mode, drop)
     logits = linear(x, params["transformer.wte.weight"], None, mode)  # tied lm_head (model.py:333)
     loss = cross_entropy(logits, labels) if labels is not None else None
     return logits, loss

@@ -13,6 +13,11 @@ Outputs (all small data files, no reference source):
                     synthetic shards (2 x 200k tokens, rng 1234), 2 loader workers.
   loader.json       sha256 of every batch the reference DataLoader yields over a grid of
                     (world, rank, workers, epoch, T, B) on synthetic ragged shards.
+  tiny_accum.json   tiny config, grad_accum=4 (loss/grad_accum, backward per micro-batch, one clip+step per 4,
+                    train_gpt2_distributed.py:404-425), 6 optimizer steps: losses, grad norms, final-param checks.
+  ddp_golden.json   the DDP identity: the reference run single-process on the concatenation of two
+                    ranks' micro-batches (L=2, C=256, H=4, V=509, T=64; 2 ranks x B=2, grad_accum=2, 3 steps,
+                    lr 1e-3): per-step loss and grad norm, and final-parameter checks, for the 2-rank tests.
 """
 from __future__ import annotations
 
@@ -57,9 +62,21 @@ def tiny_fwd_bwd():
     print("tiny loss", loss.item())
 
 
-def _ref_traj(cfg, batches, steps, grad_accum=1, lr=1e-4):
+def _param_checks(m):
+    """Final-parameter fingerprint: per-tensor sum / sum of squares, and a few tensors' leading values."""
+    out = {}
+    for n, p in m.named_parameters():
+        d = p.detach().double()
+        out[n] = {"sum": float(d.sum()), "sumsq": float((d * d).sum()),
+                  "head": [float(v) for v in p.detach().reshape(-1)[:16]]}
+    return out
+
+
+def _ref_traj(cfg, batches, steps, grad_accum=1, lr=1e-4, model_out=None):
     torch.manual_seed(42)
     m = ref_model.GPT2(cfg)
+    if model_out is not None:
+        model_out.append(m)
     opt = torch.optim.AdamW(m.parameters(), lr=lr, weight_decay=0.1, betas=(0.9, 0.95), fused=True)
     opt.zero_grad()
     losses, norms = [], []
@@ -88,6 +105,42 @@ def tiny_traj():
         json.dump({"config": TINY, "data": "np.random.default_rng(99).zipf(1.2, (20,4,65)) clipped",
                    "batch": 4, "seq_len": 64, "lr": 1e-4, "losses": losses, "grad_norms": norms}, f, indent=1)
     print("tiny traj", losses[0], losses[-1])
+
+
+def tiny_accum(steps=6, grad_accum=4):
+    cfg = ref_model.GPT2Config(**TINY)
+    rng = np.random.default_rng(17)
+    toks = (np.minimum(rng.zipf(1.2, size=(steps * grad_accum, 2, 65)), cfg.vocab_size) - 1).astype(np.int64)
+    batches = [(torch.from_numpy(t[:, :-1].copy()), torch.from_numpy(t[:, 1:].copy())) for t in toks]
+    ms = []
+    losses, norms = _ref_traj(cfg, batches, steps, grad_accum=grad_accum, lr=1e-3, model_out=ms)
+    with open(os.path.join(HERE, "tiny_accum.json"), "w") as f:
+        json.dump({"config": TINY, "data": "np.random.default_rng(17).zipf(1.2, (24,2,65)) clipped; micro-batch i "
+                   "= row i", "batch": 2, "seq_len": 64, "grad_accum": grad_accum, "steps": steps, "lr": 1e-3,
+                   "losses": losses, "grad_norms": norms, "params": _param_checks(ms[0])}, f, indent=0)
+    print("tiny accum", losses[0], losses[-1])
+
+
+DDPCFG = dict(n_layer=2, n_head=4, n_embd=256, vocab_size=509, n_positions=64, resid_pdrop=0.0, attn_pdrop=0.0)
+
+
+def ddp_golden(steps=3, grad_accum=2, world=2, per_rank=2):
+    """Single-process reference on the concatenated batch: rank r's micro-batch a of step s is
+    toks[s, a, r*per_rank:(r+1)*per_rank] (torch.Generator().manual_seed(5), the tests' generator)."""
+    cfg = ref_model.GPT2Config(**DDPCFG)
+    g = torch.Generator().manual_seed(5)
+    toks = torch.randint(0, 509, (steps, grad_accum, world * per_rank, 65), generator=g)
+    batches = [(toks[s, a, :, :-1].contiguous(), toks[s, a, :, 1:].contiguous())
+               for s in range(steps) for a in range(grad_accum)]
+    ms = []
+    losses, norms = _ref_traj(cfg, batches, steps, grad_accum=grad_accum, lr=1e-3, model_out=ms)
+    with open(os.path.join(HERE, "ddp_golden.json"), "w") as f:
+        json.dump({"config": DDPCFG, "world": world, "per_rank": per_rank, "grad_accum": grad_accum,
+                   "steps": steps, "lr": 1e-3,
+                   "data": "torch.randint(0,509,(steps,grad_accum,world*per_rank,65), Generator seed 5); rank r "
+                           "takes rows r*per_rank..", "losses": losses, "grad_norms": norms,
+                   "params": _param_checks(ms[0])}, f, indent=0)
+    print("ddp golden", losses, norms)
 
 
 def init_124m():
@@ -166,7 +219,7 @@ if __name__ == "__main__":
     ap.add_argument("--only", default="")
     a = ap.parse_args()
     jobs = {"tiny": tiny_fwd_bwd, "tinytraj": tiny_traj, "init": init_124m, "loader": loader_grid,
-            "traj": traj_124m}
+            "traj": traj_124m, "accum": tiny_accum, "ddp": ddp_golden}
     for k, fn in jobs.items():
         if a.only and k not in a.only.split(","):
             continue

@@ -1,0 +1,211 @@
+"""The reference's module surface on the HIP path (model.py:110-159,186-192,213-219,275-313,335-361):
+every sub-module callable and differentiable, the returned logits differentiable and not aliased by
+the next forward, sequence lengths that are not a multiple of the 64-token attention tile, and
+F.cross_entropy's refusal of out-of-range labels. Each result is checked against autograd of the
+oracle (oracle/model_ref.py, pinned to the reference goldens) at the precision tolerances of
+tests/test_model_gpu.py."""
+import contextlib
+import dataclasses
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+# per precision: forward rel err, grad rel err
+TOL = {"bf16": (1e-2, 3e-2), "fp32": (1e-5, 1e-4)}
+CFG = dict(n_layer=2, n_head=4, n_embd=256, vocab_size=509, n_positions=128, resid_pdrop=0.0, attn_pdrop=0.0)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def prec_ctx(prec):
+    return torch.autocast("cuda", dtype=torch.bfloat16) if prec == "bf16" else contextlib.nullcontext()
+
+
+def rel_err(a, b):
+    a, b = a.double(), b.double()
+    return float((a - b).norm() / (b.norm() + 1e-30))
+
+
+def _setup(cfg=CFG):
+    from gpt_2_distributed_amd.model import GPT2, GPT2Config
+    from oracle import model_ref
+    m = GPT2(GPT2Config(**cfg)).to(dev)
+    params = {n: p.detach().cpu().clone().requires_grad_(True) for n, p in m.named_parameters()}
+    return m, params, model_ref.Cfg(**cfg), model_ref
+
+
+def _grads_match(m, params, tol, only=None):
+    for n, p in m.named_parameters():
+        if only is not None and not n.startswith(only):
+            continue
+        ref = params[n].grad
+        if ref is None:
+            ref = torch.zeros_like(params[n])
+        g = p.grad.cpu() if p.grad is not None else torch.zeros_like(ref)
+        e = rel_err(g, ref) if ref.norm() > 0 else float(g.abs().max())
+        assert e < tol, (n, e)
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp32"])
+@pytest.mark.parametrize("T", [64, 50])
+def test_backbone_forward_backward_vs_oracle(prec, T):
+    """GPT2Backbone.forward(idx) -> the fp32 ln_f output; backprop of a custom loss through it."""
+    t_fwd, t_grad = TOL[prec]
+    m, params, rcfg, ref = _setup()
+    g = torch.Generator().manual_seed(3)
+    idx = torch.randint(0, 509, (3, T), generator=g)
+    R = torch.randn(3, T, 256, generator=g)
+    with prec_ctx(prec):
+        out = m.transformer(idx.to(dev))
+    assert out.shape == (3, T, 256) and out.dtype == torch.float32
+    (out * R.to(dev)).sum().backward()
+    r_out = ref.backbone_forward(params, rcfg, idx, prec)
+    (r_out * R).sum().backward()
+    assert rel_err(out.detach().cpu(), r_out.detach()) < t_fwd
+    _grads_match(m, params, t_grad)
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp32"])
+@pytest.mark.parametrize("kind", ["block", "mlp", "attn"])
+def test_submodule_forward_backward_vs_oracle(prec, kind):
+    """GPT2Block / MLP / CausalMultiHeadSelfAttention called on their own: output, input grad and the
+    module's parameter grads vs the oracle (model.py:213-219 / 186-192 / 110-159)."""
+    t_fwd, t_grad = TOL[prec]
+    m, params, rcfg, ref = _setup()
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(2, 64, 256, generator=g)
+    dy = torch.randn(2, 64, 256, generator=g)
+    blk = m.transformer.h[1]
+    mod = {"block": blk, "mlp": blk.mlp, "attn": blk.attn}[kind]
+    xd = x.to(dev).requires_grad_(True)
+    with prec_ctx(prec):
+        y = mod(xd)
+    y.float().backward(dy.to(dev))
+    p = {k: params["transformer.h.1." + k] for k in ref.BLOCK_KEYS}
+    xr = x.clone().requires_grad_(True)
+    fn = {"block": ref.block_forward, "mlp": ref.mlp_forward, "attn": ref.attn_forward}[kind]
+    yr = fn(xr, p, rcfg, prec, None, 1)
+    yr.backward(dy)
+    assert y.shape == yr.shape
+    assert rel_err(y.detach().float().cpu(), yr.detach()) < t_fwd
+    assert rel_err(xd.grad.cpu(), xr.grad) < t_grad
+    _grads_match(m, params, t_grad, only="transformer.h.1.")
+    # the other block got no gradient
+    assert float(m.transformer.h[0].mlp.fc1.weight.grad.abs().max()) == 0.0
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp32"])
+def test_custom_loss_on_logits(prec):
+    """model.py:351 returns differentiable logits: a loss formed by the caller on them (alone, and added
+    to the model's own loss) backpropagates through the lm_head and the whole trunk."""
+    t_fwd, t_grad = TOL[prec]
+    m, params, rcfg, ref = _setup()
+    g = torch.Generator().manual_seed(5)
+    idx = torch.randint(0, 509, (2, 64), generator=g)
+    labels = torch.randint(0, 509, (2, 64), generator=g)
+    R = torch.randn(2, 64, 509, generator=g) * 1e-2
+    for both in (False, True):
+        m.zero_grad(set_to_none=True)
+        for p in params.values():
+            p.grad = None
+        with prec_ctx(prec):
+            logits, loss = m(idx.to(dev), labels=labels.to(dev) if both else None)
+            total = (logits.float() * R.to(dev)).sum() + (loss if both else 0.0)
+        total.backward()
+        rl, rloss = ref.forward(params, rcfg, idx, labels if both else None, prec)
+        rt = (rl.float() * R).sum() + (rloss if both else 0.0)
+        rt.backward()
+        assert rel_err(logits.detach().float().cpu(), rl.detach()) < t_fwd
+        _grads_match(m, params, t_grad)
+
+
+def test_returned_logits_survive_the_next_forward():
+    """Each forward returns a fresh logits tensor (the reference returns a new tensor per call)."""
+    m, _, _, _ = _setup()
+    g = torch.Generator().manual_seed(6)
+    a = torch.randint(0, 509, (2, 64), generator=g).to(dev)
+    b = torch.randint(0, 509, (2, 64), generator=g).to(dev)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        la, _ = m(a)
+        keep = la.clone()
+        lb, _ = m(b)
+    assert torch.equal(la, keep) and not torch.equal(la, lb)
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp32"])
+@pytest.mark.parametrize("T", [1, 50, 100])
+def test_seq_len_off_the_attention_tile(prec, T):
+    """Any T <= n_positions (model.py:291), e.g. --seq_len 1000: padded inside the engine to the 64-token
+    tile; logits, loss and every gradient equal the oracle run at T (n_positions = 100, so the padded
+    positions also run past the wpe table)."""
+    t_fwd, t_grad = TOL[prec]
+    cfg = dict(CFG, n_positions=100)
+    m, params, rcfg, ref = _setup(cfg)
+    g = torch.Generator().manual_seed(7)
+    idx = torch.randint(0, 509, (3, T), generator=g)
+    labels = torch.randint(0, 509, (3, T), generator=g)
+    with prec_ctx(prec):
+        logits, loss = m(idx.to(dev), labels=labels.to(dev))
+    loss.backward()
+    rl, rloss = ref.forward(params, rcfg, idx, labels, prec)
+    rloss.backward()
+    assert logits.shape == (3, T, 509)
+    assert rel_err(logits.detach().float().cpu(), rl.detach()) < t_fwd
+    assert abs(loss.item() - rloss.item()) / rloss.item() < t_fwd
+    _grads_match(m, params, t_grad)
+    with pytest.raises(ValueError):
+        m(torch.zeros(1, 101, dtype=torch.long, device=dev))
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp32"])
+def test_out_of_range_label_poisons_the_loss(prec):
+    """F.cross_entropy raises on a label outside [0, V) (other than ignore_index); the kernel marks the
+    row NaN instead of reading past the logits row. ignore_index rows are still skipped."""
+    m, _, _, _ = _setup()
+    idx = torch.zeros(2, 64, dtype=torch.long, device=dev)
+    for bad, expect_nan in ((509, True), (-3, True), (-100, False)):
+        labels = torch.ones(2, 64, dtype=torch.long, device=dev)
+        labels[1, 5] = bad
+        with torch.no_grad(), prec_ctx(prec):
+            _, loss = m(idx, labels=labels)
+        assert bool(torch.isnan(loss)) == expect_nan, (bad, loss.item())
+
+
+def test_sub_module_outside_a_gpt2_raises():
+    from gpt_2_distributed_amd.model import GPT2Block, GPT2Config
+    blk = GPT2Block(GPT2Config(**CFG)).to(dev)
+    with pytest.raises(RuntimeError, match="sub-module of a GPT2"):
+        blk(torch.zeros(1, 64, 256, device=dev))
+
+
+def test_dropout_submodule_masks_match_the_oracle():
+    """Dropout on in a stand-alone block call: its masks are the engine's counter-based ones
+    (oracle/dropout_ref.py regenerates them from the call's seeds)."""
+    from oracle import dropout_ref
+    cfg = dict(CFG, resid_pdrop=0.1, attn_pdrop=0.1)
+    m, params, rcfg, ref = _setup(cfg)
+    m.train()
+    g = torch.Generator().manual_seed(8)
+    x = torch.randn(2, 64, 256, generator=g)
+    xd = x.to(dev).requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = m.transformer.h[0](xd)
+    seeds = m.engine().last_seeds
+    dy = torch.randn(2, 64, 256, generator=g)
+    y.backward(dy.to(dev))
+    drop = dropout_ref.step_masks(seeds, 2, 64, 256, 4, 2, 0.1, 0.1)
+    p = {k: params["transformer.h.0." + k] for k in ref.BLOCK_KEYS}
+    xr = x.clone().requires_grad_(True)
+    yr = ref.block_forward(xr, p, rcfg, "bf16", drop, 0)
+    yr.backward(dy)
+    assert rel_err(y.detach().cpu(), yr.detach()) < 1e-2
+    assert rel_err(xd.grad.cpu(), xr.grad) < 3e-2
+    _grads_match(m, params, 3e-2, only="transformer.h.0.")
+    assert dataclasses.is_dataclass(rcfg)

@@ -39,3 +39,19 @@ def test_library_exports_every_declared_symbol():
 def test_ctypes_binding_covers_the_header():
     from gpt_2_distributed_amd import _lib
     assert sorted(_lib.EXPORTED) == declared()
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libgpt2mi.so not built (run __graft_entry__.build())")
+def test_refuses_shapes_that_overflow_the_dropout_index():
+    """The counter-based dropout hashes 32-bit element / pair indices: a dropout launch whose indices
+    would wrap is refused before anything is launched (no GPU needed: argument checks only)."""
+    from gpt_2_distributed_amd import _lib
+    lib = _lib.load()
+    # attention: B*H*T*T = 256*16*1024*1024 = 2^32
+    assert lib.gpt2mi_attn_fwd(None, None, None, 256, 1024, 16, 64, 0.1, 1, None) == 22
+    assert b"32-bit dropout" in lib.gpt2mi_last_error()
+    assert lib.gpt2mi_attn_bwd(None, None, None, None, None, None, None, 256, 1024, 16, 64, 0.1, 1, None) == 22
+    # GEMM epilogue dropout: M*N = 2^20 * 2^13 = 2^33 pairs*2
+    assert lib.gpt2mi_gemm(0, 2, 1 << 20, 1 << 13, 64, None, 64, None, 64, None, 1 << 13, None, None, None, 0,
+                           1.0, None, 0, 1, 0.1, 1, None, None) == 22
+    assert b"32-bit dropout" in lib.gpt2mi_last_error()

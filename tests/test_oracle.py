@@ -143,3 +143,41 @@ def test_dropout_restatement():
     l0, _ = model_ref.forward(params, TINY, idx, None, "fp32")
     l1, _ = model_ref.forward(params, TINY, idx, None, "fp32", drop=ones)
     assert torch.equal(l0, l1)
+
+
+def _check_params(params, ref, rtol):
+    for n, p in params.items():
+        r = ref[n]
+        d = p.detach().double()
+        assert abs(float(d.sum()) - r["sum"]) <= rtol * max(1.0, float(d.abs().sum())), n
+        assert abs(float((d * d).sum()) - r["sumsq"]) <= rtol * r["sumsq"] + 1e-12, n
+        np.testing.assert_allclose(p.detach().reshape(-1)[:16].numpy(), r["head"], rtol=rtol, atol=1e-6, err_msg=n)
+
+
+def test_grad_accumulation_matches_reference():
+    """train_ref.run with grad_accum=4 (loss/grad_accum per micro-batch, one clip+AdamW per 4:
+    train_gpt2_distributed.py:404-425) vs the reference loop's trajectory (tests/golden/tiny_accum.json)."""
+    ref = json.load(open(os.path.join(GOLDEN, "tiny_accum.json")))
+    rng = np.random.default_rng(17)
+    toks = (np.minimum(rng.zipf(1.2, size=(24, 2, 65)), TINY.vocab_size) - 1).astype(np.int64)
+    batches = [(torch.from_numpy(t[:, :-1].copy()), torch.from_numpy(t[:, 1:].copy())) for t in toks]
+    params = model_ref.init_params(TINY)
+    losses, norms = train_ref.run(TINY, batches, 6, grad_accum=4, lr=1e-3, params=params)
+    np.testing.assert_allclose(losses, ref["losses"], rtol=1e-4)
+    np.testing.assert_allclose(norms, ref["grad_norms"], rtol=1e-3)
+    _check_params(params, ref["params"], 1e-4)
+
+
+def test_ddp_golden_is_the_concatenated_batch_run():
+    """tests/golden/ddp_golden.json (the reference on the 2-rank concatenated batch) is what the oracle
+    computes from the same per-rank micro-batches, concatenated in rank order."""
+    ref = json.load(open(os.path.join(GOLDEN, "ddp_golden.json")))
+    cfg = model_ref.Cfg(**ref["config"])
+    S, GA, W, P = ref["steps"], ref["grad_accum"], ref["world"], ref["per_rank"]
+    toks = torch.randint(0, 509, (S, GA, W * P, 65), generator=torch.Generator().manual_seed(5))
+    batches = [(toks[s, a, :, :-1].contiguous(), toks[s, a, :, 1:].contiguous()) for s in range(S) for a in range(GA)]
+    params = model_ref.init_params(cfg)
+    losses, norms = train_ref.run(cfg, batches, S, grad_accum=GA, lr=ref["lr"], params=params)
+    np.testing.assert_allclose(losses, ref["losses"], rtol=1e-4)
+    np.testing.assert_allclose(norms, ref["grad_norms"], rtol=1e-3)
+    _check_params(params, ref["params"], 1e-4)

@@ -1,7 +1,9 @@
-"""Multi-process data-parallel logic on CPU with gloo (world size 2): the bucketed gradient
-all-reduce over a flat arena (DDP path) and the reduce-scatter/all-gather sharding (fsdp path).
-The identity checked is the one the DDP golden rests on: averaging per-rank grads of
-equal-size batches equals the single-process grad of the concatenated batch."""
+"""Multi-process data-parallel logic on CPU with gloo (world sizes 2 and 3): the bucketed SUM
+all-reduce over a flat arena (DDP path), the FSDP shard plan (any world size) and its bf16/fp32
+reduce-scatter / all-gather round trip. Gradients reach the collectives pre-divided by world (the
+engine's GradHooks.begin_backward), so a SUM is the average on every backend; the identity the DDP
+golden rests on is then: the mean of per-rank grads of equal-size batches equals the
+single-process grad of the concatenated batch (tests/test_ddp_gpu.py checks it against the reference)."""
 import os
 import socket
 import tempfile
@@ -48,7 +50,7 @@ def _bucketed(rank, world):
     from gpt_2_distributed_amd.parallel import BucketedReducer
     n = 10_000
     g = torch.Generator().manual_seed(rank)
-    flat = torch.randn(n, generator=g)
+    flat = torch.randn(n, generator=g) / world  # what a synced backward hands over: grads pre-divided by world
     expect = sum(torch.randn(n, generator=torch.Generator().manual_seed(r)) for r in range(world)) / world
     # ranges become final in descending arena order (like blocks L-1 .. 0, then the embeddings)
     bounds = [0, 1000, 2500, 4000, 7000, 9000, n]
@@ -56,38 +58,81 @@ def _bucketed(rank, world):
     red = BucketedReducer(flat, order, bucket_mb=3000 * 4 / 2**20)
     for name, _, _ in order[:3]:
         red.mark_ready(name)
-    n_launched = len(red.works)
-    red.flush()
-    return (torch.allclose(flat, expect, atol=1e-6), n_launched)
+    n_launched = red.launched
+    red.finish()
+    return (torch.allclose(flat, expect, atol=1e-6), n_launched, red.launched == 0 and red.next == 0)
 
 
 def test_bucketed_allreduce_gloo():
     out = _spawn(_bucketed)
     for r, v in out.items():
         assert isinstance(v, tuple), v
-        ok, n_launched = v
+        ok, n_launched, was_reset = v
         assert ok
-        assert n_launched >= 1  # buckets left before the flush (overlap with the rest of backward)
+        assert n_launched >= 1  # buckets issued before finish (they overlap the rest of the backward)
+        assert was_reset        # finish() leaves the reducer ready for the next backward
+
+
+def test_backward_ready_order_is_contiguous():
+    """The engine's ready events (head, h.L-1 .. h.0, embed) tile the arena contiguously in reverse order."""
+    from gpt_2_distributed_amd.model import GPT2, GPT2Config
+    from gpt_2_distributed_amd.parallel import backward_order, unit_ranges
+    m = GPT2(GPT2Config(n_layer=3, n_head=2, n_embd=128, vocab_size=509, n_positions=64))
+    units = unit_ranges(m.layout, 3)
+    assert [u[0] for u in units] == ["embed", "h.0", "h.1", "h.2", "head"]
+    assert units[0][1] == 0 and units[-1][2] == m.layout.total
+    for (_, _, hi), (_, lo, _) in zip(units, units[1:]):
+        assert hi == lo
+    order = backward_order(units)
+    assert [u[0] for u in order] == ["head", "h.2", "h.1", "h.0", "embed"]
+    # every parameter lies in exactly one unit, and each block's 12 tensors in its own
+    for n, sl in m.layout.slots.items():
+        owners = [u for u, lo, hi in units if lo <= sl.offset < hi]
+        assert len(owners) == 1
+        if n.startswith("transformer.h."):
+            assert owners[0] == "h." + n.split(".")[2]
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 6, 8, 32])
+def test_shard_plan_any_world_size(world):
+    """FSDP shard plan: every unit splits into `world` aligned equal chunks covering it (zero padding
+    past its end), for world sizes with odd factors too (3, 6, 12 ...)."""
+    from gpt_2_distributed_amd.model import GPT2, GPT2Config
+    from gpt_2_distributed_amd.parallel import SHARD_ALIGN, plan_shards, unit_ranges
+    m = GPT2(GPT2Config(n_layer=2, n_head=2, n_embd=128, vocab_size=509, n_positions=64))
+    plans, total = plan_shards(unit_ranges(m.layout, 2), world)
+    off = 0
+    for p in plans:
+        assert p.per % SHARD_ALIGN == 0 and p.per * world >= p.n > p.per * (world - 1) - SHARD_ALIGN * world
+        assert p.soff == off
+        off += p.per
+    assert total == off
 
 
 def _shard_math(rank, world):
-    total = 1000
-    per = (total + world - 1) // world
-    per = (per + 63) // 64 * 64
-    padded = per * world
-    g = torch.arange(padded, dtype=torch.float32) * (rank + 1)
-    shard = torch.empty(per)
-    dist.reduce_scatter_tensor(shard, g, op=dist.ReduceOp.SUM)
-    shard /= world
-    exp = torch.arange(padded, dtype=torch.float32)[rank * per:(rank + 1) * per] * sum(range(1, world + 1)) / world
-    full = torch.empty(padded)
-    dist.all_gather_into_tensor(full, shard)
-    exp_full = torch.arange(padded, dtype=torch.float32) * sum(range(1, world + 1)) / world
-    return bool(torch.allclose(shard, exp) and torch.allclose(full, exp_full))
+    """The FSDP collective pattern of one unit, in both reduce/param dtypes: a unit of n elements packed
+    (zero-padded) to world*per, reduce-scattered (SUM of world-pre-divided grads) into this rank's per
+    chunk, and the chunks all-gathered back: the first n elements are the average, in unit order."""
+    from gpt_2_distributed_amd.parallel import plan_shards
+    ok = True
+    n = 1000
+    (p,), _ = plan_shards([("u", 0, n)], world)
+    for dt in (torch.float32, torch.bfloat16):
+        g = torch.zeros(p.per * world, dtype=dt)
+        g[:n] = (torch.arange(n, dtype=torch.float32) % 64 * (rank + 1) / world).to(dt)
+        shard = torch.empty(p.per, dtype=dt)
+        dist.reduce_scatter_tensor(shard, g, op=dist.ReduceOp.SUM)
+        full = torch.empty(p.per * world, dtype=dt)
+        dist.all_gather_into_tensor(full, shard)
+        exp = (torch.arange(n, dtype=torch.float32) % 64) * sum(range(1, world + 1)) / world
+        tol = 1e-6 if dt == torch.float32 else 2e-2
+        ok &= bool(torch.allclose(full[:n].float(), exp, rtol=tol, atol=tol)) and bool((full[n:] == 0).all())
+    return ok
 
 
-def test_reduce_scatter_all_gather_gloo():
-    out = _spawn(_shard_math)
+@pytest.mark.parametrize("world", [2, 3])
+def test_reduce_scatter_all_gather_gloo(world):
+    out = _spawn(_shard_math, world)
     assert all(v is True for v in out.values()), out
 
 

@@ -63,12 +63,53 @@ def test_checkpoint_resume_matches_uninterrupted_run(tmp_path):
 
     m2 = GPT2(GPT2Config(**TINY)).to(dev)  # same seed-42 init; overwritten by the checkpoint
     opt2 = m2.configure_optimizers(learning_rate=1e-3)
-    assert load_checkpoint(m2, opt2, ck) == 2
+    assert load_checkpoint(m2, opt2, ck)["step"] == 2
     losses = [_step(m2, opt2, b) for b in bs[2:]]
     for a, b in zip(losses, ref_losses):
         assert abs(a - b) <= 1e-6 * abs(b)
     for k, v in m2.named_parameters():
         assert (v - ref_params[k]).abs().max().item() <= 1e-6, k
+
+
+def test_checkpoint_resume_restores_the_dropout_stream(tmp_path):
+    """Dropout on (p = 0.1): the resumed run draws the same masks as the uninterrupted one (the engine's
+    dropout stream position is saved in trainer.json and restored)."""
+    from gpt_2_distributed_amd.model import GPT2, GPT2Config
+    from gpt_2_distributed_amd.train_gpt2_distributed import load_checkpoint, save_checkpoint
+    cfg = dict(TINY, resid_pdrop=0.1, attn_pdrop=0.1)
+    bs = _batches(4)
+    m = GPT2(GPT2Config(**cfg)).to(dev)
+    opt = m.configure_optimizers(learning_rate=1e-3)
+    for b in bs[:2]:
+        _step(m, opt, b)
+    ck = save_checkpoint(m, opt, 2, str(tmp_path), {"epoch": 0, "micro": 2})
+    ref_losses = [_step(m, opt, b) for b in bs[2:]]
+    m2 = GPT2(GPT2Config(**cfg)).to(dev)
+    opt2 = m2.configure_optimizers(learning_rate=1e-3)
+    st = load_checkpoint(m2, opt2, ck)
+    assert (st["step"], st["epoch"], st["micro"]) == (2, 0, 2)
+    losses = [_step(m2, opt2, b) for b in bs[2:]]
+    for a, b in zip(losses, ref_losses):
+        assert abs(a - b) <= 1e-6 * abs(b)
+
+
+def test_trainer_cli_resume_skips_consumed_batches(tmp_path):
+    """--resume continues the data stream where the checkpoint left it: 2 steps + resume for 2 more logs
+    the same losses as 4 uninterrupted steps (dropout 0.1, 2 micro-batches per step)."""
+    data = tmp_path / "data"
+    base = [sys.executable, "-m", "gpt_2_distributed_amd.train_gpt2_distributed", "--data_dir", str(data),
+            "--synthetic", "2", "--synthetic_tokens", "60000", "--seq_len", "128", "--batch", "4",
+            "--grad_accum_steps", "2", "--workers", "1", "--log_every", "1", "--training_mode", "local"]
+    r = subprocess.run(base + ["--max_steps", "4", "--save_every", "2", "--save_dir", str(tmp_path / "a")], cwd=REPO,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    full = [json.loads(l)["loss"] for l in r.stdout.splitlines() if l.startswith("{")]
+    r = subprocess.run(base + ["--max_steps", "4", "--save_every", "100", "--save_dir", str(tmp_path / "b"),
+                               "--resume", str(tmp_path / "a" / "step_0000002")], cwd=REPO, capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    resumed = {json.loads(l)["step"]: json.loads(l)["loss"] for l in r.stdout.splitlines() if l.startswith("{")}
+    assert abs(resumed[3] - full[2]) <= 1e-4 * full[2] and abs(resumed[4] - full[3]) <= 1e-4 * full[3]
 
 
 def test_trainer_cli_end_to_end(tmp_path):
