@@ -189,7 +189,7 @@ class _TrunkFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, engine, idx, *params):
         ctx.set_materialize_grads(False)
-        out = engine._trunk_forward_module(idx)
+        out = engine._trunk_forward_module(idx, True)
         ctx.engine = engine
         ctx.token = engine._fwd_token
         ctx.n_params = len(params)
@@ -210,7 +210,7 @@ class _SubFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, engine, kind, layer, x, *params):
         ctx.set_materialize_grads(False)
-        y, state = engine._sub_forward(kind, layer, x)
+        y, state = engine._sub_forward(kind, layer, x, True)
         ctx.engine, ctx.kind, ctx.layer, ctx.state, ctx.n_params = engine, kind, layer, state, len(params)
         ctx.x_dtype = x.dtype
         return y
@@ -381,6 +381,8 @@ class Engine:
                                    "set_to_none=True or the model's optimizer before backward")
 
     def _begin_grads(self, act) -> float:
+        if act == BF16 and self.param_provider is None and self._shadowT_stale:
+            self.refresh_shadowT()  # the dgrads read W^T (a forward run without grad did not build it)
         self._prepare_grads()
         self.bwd_act = act  # the precision of this backward's gradients (FSDP reduces in it)
         scale = self.grad_sync.begin_backward() if self.grad_sync is not None else 1.0
@@ -440,17 +442,18 @@ class Engine:
         with torch.no_grad():
             return self._forward(idx, labels, False)
 
+    # (autograd.Function.forward runs with grad mode off: whether a backward will follow is decided here)
     def backbone_forward(self, idx: torch.Tensor) -> torch.Tensor:
         if self._grad_enabled():
             return _TrunkFn.apply(self, idx, *self._params)
         with torch.no_grad():
-            return self._trunk_forward_module(idx)
+            return self._trunk_forward_module(idx, False)
 
     def sub_forward(self, kind: str, layer: int, x: torch.Tensor) -> torch.Tensor:
         if self._grad_enabled() or x.requires_grad:
             return _SubFn.apply(self, kind, layer, x, *self._params)
         with torch.no_grad():
-            return self._sub_forward(kind, layer, x)[0]
+            return self._sub_forward(kind, layer, x, False)[0]
 
     # ---- shared kernel sequences --------------------------------------------------------------------
     def _dropout(self):
@@ -687,11 +690,11 @@ class Engine:
         self._end_grads()
 
     # ---- GPT2Backbone.forward on its own -------------------------------------------------------------
-    def _trunk_forward_module(self, idx):
+    def _trunk_forward_module(self, idx, need_grad):
         idx, _, T = self._pad(idx, None)
         B, Tp = idx.shape
         act = self.compute_dtype()
-        self._sync_shadows(act, self._grad_enabled())
+        self._sync_shadows(act, need_grad)
         ws = self.workspace(B, Tp, act)
         pr, pa = self._dropout()
         seeds = self._next_seeds()
@@ -719,7 +722,7 @@ class Engine:
         self._end_grads()
 
     # ---- GPT2Block / MLP / CausalMultiHeadSelfAttention forward on their own --------------------------
-    def _sub_forward(self, kind, l, x):
+    def _sub_forward(self, kind, l, x, need_grad):
         """kind: "block" (x = residual stream, model.py:213-219), "mlp" (x = ln2 output, model.py:186-192),
         "attn" (x = ln1 output, model.py:110-159). Returns (y, saved state)."""
         cfg = self.cfg
@@ -734,7 +737,7 @@ class Engine:
         Tp = padded_len(T)
         M = B * Tp
         act = self.compute_dtype()
-        self._sync_shadows(act, self._grad_enabled())
+        self._sync_shadows(act, need_grad)
         xf = x.to(F32)
         if Tp != T:
             xf = F.pad(xf, (0, 0, 0, Tp - T))
