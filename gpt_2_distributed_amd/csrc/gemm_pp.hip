@@ -86,6 +86,23 @@ __device__ __forceinline__ void dma_half(const bf16* __restrict__ src, int ld, i
   }
 }
 
+// The same half-tile of a k-contiguous operand by BUFFER LDS-DMA (the persistent kernel): the lane part of
+// the source offset, row (l >> 3) of an instruction's 8 rows and 16-B chunk (l & 7) ^ (l >> 3), is the same
+// for every instruction, half and tile (one VGPR per operand); the row-group / K-tile position is a
+// wave-uniform byte offset (soffset). Rows past the operand's end read as zeros (buffer range check).
+__device__ __forceinline__ uint32_t kc_lane_off(int ld, int lane) {
+  return (uint32_t)(((lane >> 3) * ld + 8 * ((lane & 7) ^ (lane >> 3))) * (int)sizeof(bf16));
+}
+__device__ __forceinline__ void dma_half_buf(__amdgpu_buffer_rsrc_t rs, int ld, int row0, int k0, uint32_t loff,
+                                             char* slot, int wid) {
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int ins = wid * 2 + t;
+    const int soff = ((row0 + 8 * ins) * ld + k0) * (int)sizeof(bf16);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(slot + ins * 1024), 16, loff, soff, 0, 0);
+  }
+}
+
 // fragment reads: lane gets operand[ir0 + (l&15)][32kk + 8(l>>4) + 0..7]
 template <bool TRANS>
 __device__ __forceinline__ bf16x8 frag(const char* slot, int ir0, int kk, int lane) {
@@ -178,10 +195,26 @@ __device__ __forceinline__ void lds_barrier() {
 #define PP_STAMP(I)
 #endif
 
-template <bool A_T, bool B_T, int EPI, int MAP>
+// Output tile of item `pid` (GM M-tiles per group share their B tiles in L2).
+__device__ __forceinline__ void tile_of(int pid, int tiles_m, int tiles_n, int& m0, int& n0) {
+  constexpr int GM = 4;
+  const int group = pid / (GM * tiles_n);
+  const int first_m = group * GM;
+  const int gsz = min(tiles_m - first_m, GM);
+  m0 = (first_m + (pid % (GM * tiles_n)) % gsz) * BM;
+  n0 = ((pid % (GM * tiles_n)) / gsz) * BN;
+}
+
+// PERSIST: one block per CU walks the output tiles (item = remap(blockIdx + i * gridDim)); at each tile
+// boundary the NEXT tile's first K-tile is staged by LDS-DMA into buffer 0 while this tile's epilogue runs
+// through buffer 1 (a 64-row fp32 image, four passes), so the operand latency of a tile start and the
+// block launch gap overlap the epilogue instead of following it (the K = 768 shapes spend ~8 us of ~25
+// per tile there). Layout-0 shapes without split-K only (host-selected).
+template <bool A_T, bool B_T, int EPI, int MAP, bool PERSIST = false>
 __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   PP_STAMP(0)
   constexpr bool AIL = MAP & 1, BIL = MAP & 2;  // interleaved half-tile maps (A/B experiments)
+  static_assert(!PERSIST || MAP == 0, "the persistent epilogue assumes the contiguous half-tile map");
   __shared__ __attribute__((aligned(1024))) char smem[kLds];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -191,37 +224,53 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   const int ntiles = tiles_m * tiles_n;
   // 1-D grid over (split, tile) items, split-major: the XCD remap gives each XCD a contiguous item range,
   // so the blocks of one K split (which share its A and B token rows) run out of one L2
-  const int nsplit = (P.K + P.k_per_split - 1) / P.k_per_split;
-  const int item = xcd_remap(blockIdx.x, ntiles * nsplit);
+  const int nsplit = PERSIST ? 1 : (P.K + P.k_per_split - 1) / P.k_per_split;
+  int vid = blockIdx.x;  // PERSIST: virtual block id of this tile (blockIdx + i * gridDim, same XCD label)
+  const int item = xcd_remap(vid, ntiles * nsplit);
   const int split = item / ntiles;
-  const int pid = item - split * ntiles;
-  constexpr int GM = 4;
-  const int group = pid / (GM * tiles_n);
-  const int first_m = group * GM;
-  const int gsz = min(tiles_m - first_m, GM);
-  const int tm = first_m + (pid % (GM * tiles_n)) % gsz;
-  const int tn = (pid % (GM * tiles_n)) / gsz;
-  const int m0 = tm * BM, n0 = tn * BN;
+  int m0, n0;
+  tile_of(item - split * ntiles, tiles_m, tiles_n, m0, n0);
   const int kbeg = split * P.k_per_split;
   const int nk = (min(P.K, kbeg + P.k_per_split) - kbeg) / BK;  // even (host-checked)
 
   f32x4 acc[2][2][4][2];
+  auto zero_acc = [&]() {
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < 2; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+      for (int b = 0; b < 2; ++b)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+          for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  zero_acc();
 
   auto kofs = [&](int t) { return kbeg + t * BK; };
-  auto dma_a = [&](int t, int h, char* buf) {
-    dma_half<A_T, true, AIL>(P.A, P.lda, m0, h, kofs(t), P.M - 1, buf + (h ? SA1 : SA0), wid, lane);
+  // PERSIST (k-contiguous A and B): buffer DMA, 2 lane-offset VGPRs for every tile instead of per-tile
+  // 64-bit row pointers (the persistent loop keeps its registers under the 256 of 2 waves/SIMD)
+  [[maybe_unused]] __amdgpu_buffer_rsrc_t rs_a, rs_b;
+  [[maybe_unused]] uint32_t loff_a = 0, loff_b = 0;
+  if constexpr (PERSIST) {
+    rs_a = __builtin_amdgcn_make_buffer_rsrc((void*)P.A, 0, 0x7fffffff, 0x00020000);
+    rs_b = __builtin_amdgcn_make_buffer_rsrc((void*)P.B, 0, 0x7fffffff, 0x00020000);
+    loff_a = kc_lane_off(P.lda, lane);
+    loff_b = kc_lane_off(P.ldb, lane);
+  }
+  auto dma_a_at = [&](int mm0, int t, int h, char* buf) {
+    if constexpr (PERSIST)
+      dma_half_buf(rs_a, P.lda, mm0 + (h << 7), kofs(t), loff_a, buf + (h ? SA1 : SA0), wid);
+    else
+      dma_half<A_T, true, AIL>(P.A, P.lda, mm0, h, kofs(t), P.M - 1, buf + (h ? SA1 : SA0), wid, lane);
   };
-  auto dma_b = [&](int t, int h, char* buf) {
-    dma_half<B_T, false, BIL>(P.B, P.ldb, n0, h, kofs(t), P.N - 1, buf + (h ? SB1 : SB0), wid, lane);
+  auto dma_b_at = [&](int nn0, int t, int h, char* buf) {
+    if constexpr (PERSIST)
+      dma_half_buf(rs_b, P.ldb, nn0 + (h << 7), kofs(t), loff_b, buf + (h ? SB1 : SB0), wid);
+    else
+      dma_half<B_T, false, BIL>(P.B, P.ldb, nn0, h, kofs(t), P.N - 1, buf + (h ? SB1 : SB0), wid, lane);
   };
+  auto dma_a = [&](int t, int h, char* buf) { dma_a_at(m0, t, h, buf); };
+  auto dma_b = [&](int t, int h, char* buf) { dma_b_at(n0, t, h, buf); };
   char* buf0 = smem;
   char* buf1 = smem + kBuf;
 
@@ -237,6 +286,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   PP_STAMP(1)
   if (wr == 1) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind group 0
   __builtin_amdgcn_sched_barrier(0);
+  for (;;) {  // PERSIST: one iteration per output tile (non-persistent: exactly one)
 
   Frags fr;
   // One K-tile (4 phases) of the pair starting at t: S = 0 / 1 is the tile's parity. In the last pair
@@ -281,19 +331,92 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   __builtin_amdgcn_sched_barrier(0);
   PP_STAMP(2)
 
-  // ---- epilogue: acc[mi][ni][i][j][r] = C[m0 + mi*128 + wr*64 + 16i + (l&15)][n0 + ni*128 + wc*32 + 16j + 4(l>>4) + r]
-  float alpha = P.alpha;
-  if (P.alpha_dev) alpha *= P.alpha_dev[0];
-  float* img = reinterpret_cast<float*>(smem);  // [128][256] fp32, 1 KiB rows
   const int tid = threadIdx.x;
   const int ch = tid & 63;
   const int gn = n0 + 4 * ch;
   const f32x4 bias = (P.bias && EPI != EPI_GELU_BWD) ? *reinterpret_cast<const f32x4*>(P.bias + gn)
                                                      : f32x4{0.f, 0.f, 0.f, 0.f};
+  // PERSIST: the next tile's K-tile 0 goes into buffer 0 now (last read in this tile's final even K-tile,
+  // several barriers ago); the epilogue image lives in buffer 1. The bias is waited for first: hipcc waits
+  // vmcnt(0) at the first use of an ordinary load while an LDS-DMA is in flight, which would drain the
+  // next tile's DMAs inside the epilogue (the persistent path is only selected for epilogues without
+  // other operand loads: BF16, GELU).
+  int next_m0 = 0, next_n0 = 0;
+  bool has_next = false;
+  if constexpr (PERSIST) {
+    asm volatile("" ::"v"(bias[0]), "v"(bias[1]), "v"(bias[2]), "v"(bias[3]));
+    vid += gridDim.x;
+    has_next = vid < ntiles;
+    if (has_next) {
+      tile_of(xcd_remap(vid, ntiles), tiles_m, tiles_n, next_m0, next_n0);
+      dma_a_at(next_m0, 0, 0, buf0);
+      dma_b_at(next_n0, 0, 0, buf0);
+      dma_b_at(next_n0, 0, 1, buf0);
+      dma_a_at(next_m0, 0, 1, buf0);
+    }
+  }
+
+  // ---- epilogue: acc[mi][ni][i][j][r] = C[m0 + mi*128 + wr*64 + 16i + (l&15)][n0 + ni*128 + wc*32 + 16j + 4(l>>4) + r]
+  float alpha = P.alpha;
+  if (P.alpha_dev) alpha *= P.alpha_dev[0];
+  // [128][256] fp32 image (1 KiB rows) over the whole LDS; PERSIST: [64][256] in buffer 1
+  float* img = reinterpret_cast<float*>(PERSIST ? buf1 : smem);
   constexpr bool kOpnd = EPI == EPI_RESID || EPI == EPI_GELU_BWD || EPI == EPI_F32;
-  constexpr bool kCsum = EPI == EPI_BF16 || EPI == EPI_GELU_BWD;  // fused bias grad of the stored output
+  // fused bias grad of the stored output (never selected with the persistent schedule)
+  constexpr bool kCsum = !PERSIST && (EPI == EPI_BF16 || EPI == EPI_GELU_BWD);
   const bool csum_on = kCsum && P.dbias != nullptr;
   f32x4 csum = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (PERSIST) {
+    // four 64-row passes: pass q = 2*mi + g holds rows q*64.. (the 16-row groups of waves with wr == g)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int mi = q >> 1, g = q & 1;
+      f32x4 opnd[8];
+      if constexpr (kOpnd) {
+#pragma unroll
+        for (int it = 0; it < 8; ++it) opnd[it] = epilogue_operand<EPI>(P, min(m0 + q * 64 + it * 8 + wid, P.M - 1), gn);
+      }
+      if (q) lds_barrier();  // the previous pass's reads are done before this pass overwrites the image
+      if (wr == g) {
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const int r = 16 * i + (lane & 15);
+              const int c = ni * 32 + wc * 8 + 4 * j + (lane >> 4);
+              f32x4 v = acc[mi][ni][i][j];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] *= alpha;
+              *reinterpret_cast<f32x4*>(img + r * 256 + 4 * (c ^ (r & 15))) = v;
+            }
+      }
+      lds_barrier();
+      f32x4 v[8];
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const int r = it * 8 + wid;
+        v[it] = *reinterpret_cast<const f32x4*>(img + r * 256 + 4 * (ch ^ (r & 15)));
+      }
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const int gm = m0 + q * 64 + it * 8 + wid;
+        if (gm < P.M) {
+          f32x4 w = v[it];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) w[e] += bias[e];
+          const f32x4 o = epilogue_apply<EPI>(P, gm, gn, w, kOpnd ? opnd[it] : f32x4{0.f, 0.f, 0.f, 0.f});
+          if constexpr (kCsum) {
+            if (csum_on) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) csum[e] += o[e];
+            }
+          }
+        }
+      }
+    }
+  } else {
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi) {
     // the pass's epilogue operands (residual / pre-activation / old C): all 16 loads in flight
@@ -360,6 +483,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
       }
     }
   }
+  }  // non-persistent epilogue
   if constexpr (kCsum) {
     if (csum_on) {  // the 8 waves hold partial sums of the same 256 columns: reduce in LDS, 1 atomic/column
       lds_barrier();  // every wave has finished reading the staging image
@@ -374,6 +498,25 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
     }
   }
   PP_STAMP(3)
+  if constexpr (!PERSIST) {
+    return;
+  } else {
+    if (!has_next) return;
+    // the next tile's prologue continues: A_0 / B_0 of its K-tile 1 into buffer 1 once every wave is done
+    // with the image there, then the same counted wait as the first prologue (epilogue stores issued in
+    // between only make it wait longer, never too little: outstanding <= 8 leaves >= 4 DMAs retired)
+    lds_barrier();
+    m0 = next_m0;
+    n0 = next_n0;
+    zero_acc();
+    dma_a(1, 0, buf1);
+    dma_b(1, 0, buf1);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (wr == 1) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  }  // tile loop
 }
 
 // Default half-tile maps: interleaved for m-contiguous (transposed) operands, contiguous otherwise
@@ -384,6 +527,27 @@ int launch(const GemmParams& P, hipStream_t s, int splits) {
   dim3 grid(((P.M + BM - 1) / BM) * (P.N / BN) * splits);
   gemm_pp_kernel<A_T, B_T, EPI, MAP><<<grid, kThreads, 0, s>>>(P);
   return gpt2mi::check_launch("gemm_pp");
+}
+
+int num_cus() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || n <= 0)
+      n = 256;
+    n = n / 8 * 8;  // a multiple of the 8 XCDs keeps every block's virtual ids on one XCD label
+  }
+  return n;
+}
+
+// persistent variant: one block per CU, grid a multiple of 8
+template <int EPI>
+int launch_persistent(const GemmParams& P, hipStream_t s) {
+  const int ntiles = ((P.M + BM - 1) / BM) * (P.N / BN);
+  dim3 grid(min(ntiles, num_cus()));
+  gemm_pp_kernel<false, false, EPI, 0, true><<<grid, kThreads, 0, s>>>(P);
+  return gpt2mi::check_launch("gemm_pp_persistent");
 }
 
 }  // namespace
@@ -407,6 +571,15 @@ int gemm_pp_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t 
       if (map == 3) return launch<false, true, EPI_BF16, 3>(P, s, 1);
     }
   }
+  // short-K forward-layout shapes with no epilogue operand loads: the persistent schedule (map < 0 forces
+  // the one-tile-per-block kernel, tools/gemm_probe.py A/B)
+  const int ntiles = ((P.M + BM - 1) / BM) * (P.N / BN);
+  if (layout == 0 && map == 0 && P.K <= 1024 && ntiles >= 2 * num_cus() && P.dbias == nullptr &&
+      (epilogue == EPI_BF16 || epilogue == EPI_GELU) && P.M % BM == 0 && (size_t)P.M * P.lda * 2 < (1ull << 31) &&
+      (size_t)P.N * P.ldb * 2 < (1ull << 31)) {
+    return epilogue == EPI_BF16 ? launch_persistent<EPI_BF16>(P, s) : launch_persistent<EPI_GELU>(P, s);
+  }
+  if (map < 0) map = 0;
   switch (layout * 16 + epilogue) {
     case 0 * 16 + EPI_BF16: return launch<false, false, EPI_BF16>(P, s, 1);
     case 0 * 16 + EPI_F32: return launch<false, false, EPI_F32>(P, s, 1);

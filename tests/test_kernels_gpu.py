@@ -504,3 +504,39 @@ def test_transpose_bf16_batched():
         w = src[off:off + r * c].view(r, c)
         assert torch.equal(dst[off:off + r * c].view(c, r), w.t()), (r, c)
         assert torch.all(dst[off + r * c:off + r * c + 64] == 7.0)
+
+
+@pytest.mark.parametrize("epi", ["plain", "bias", "gelu_drop"])
+@pytest.mark.parametrize("M,N", [(8192, 4096), (65536, 2304)])
+def test_gemm_persistent_schedule_bitwise(epi, M, N):
+    """The persistent ping-pong schedule (short-K forward-layout GEMMs with >= 2 tiles per CU: one block per CU
+    walks the tiles, the next tile's first K-tile lands during this tile's epilogue) computes every output
+    element exactly as the one-tile-per-block kernel (gpt2mi_set_gemm_impl(6) forces that one): bitwise equal,
+    and within bf16 rounding of an fp32 reference on sampled rows."""
+    K = 768
+    g = torch.Generator().manual_seed(M + N)
+    A = bf(torch.randn(M, K, generator=g)).to(dev)
+    W = bf(torch.randn(N, K, generator=g) * 0.05).to(dev)
+    bias = torch.randn(N, generator=g).to(dev) if epi != "plain" else None
+    outs = []
+    for impl in (0, 6):
+        L().set_gemm_impl(impl)
+        try:
+            C = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+            if epi == "gelu_drop":
+                aux = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+                L().gemm(0, L().EPI_GELU, M, N, K, A, K, W, K, C, N, bias=bias, aux=aux, ldaux=N, p_drop=0.1,
+                         seed=99)
+                outs.append((C, aux))
+            else:
+                L().gemm(0, L().EPI_BF16, M, N, K, A, K, W, K, C, N, bias=bias)
+                outs.append((C,))
+        finally:
+            L().set_gemm_impl(0)
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    rows = torch.arange(0, M, M // 64, device=dev)
+    ref = A[rows].float() @ W.float().t() + (bias if bias is not None else 0.0)
+    if epi != "gelu_drop":
+        assert rel_err(outs[0][0][rows].float().cpu(), ref.cpu()) < 4e-3

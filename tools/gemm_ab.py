@@ -1,0 +1,61 @@
+#!/usr/bin/env python
+"""A/B of GEMM schedules on the GPT-2 124M step shapes (B=64, T=1024): gpt2mi_set_gemm_impl variants timed in
+interleaved rounds with HIP events (random data).  python tools/gemm_ab.py [impl_a impl_b ...]  (default 0 6:
+the persistent ping-pong schedule vs the one-tile-per-block kernel)."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from gpt_2_distributed_amd import _lib as K  # noqa: E402
+
+dev = "cuda"
+PEAK = 2516.6
+
+
+def main():
+    impls = [int(a) for a in sys.argv[1:]] or [0, 6]
+    M, C, Vp = 65536, 768, 50432
+    g = torch.Generator(device=dev).manual_seed(0)
+    rnd = lambda *s, sc=1.0: (torch.randn(*s, device=dev, generator=g) * sc).to(torch.bfloat16)  # noqa: E731
+    x = rnd(M, C)
+    shapes = {
+        "lm_head fwd": (Vp, None, K.EPI_BF16),
+        "qkv fwd +bias": (3 * C, True, K.EPI_BF16),
+        "fc1 fwd gelu+drop": (4 * C, True, K.EPI_GELU),
+    }
+    bufs = {}
+    for name, (N, has_bias, epi) in shapes.items():
+        W = rnd(N, C, sc=0.05)
+        bias = torch.randn(N, device=dev) if has_bias else None
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+        aux = torch.empty(M, N, dtype=torch.bfloat16, device=dev) if epi == K.EPI_GELU else None
+        bufs[name] = (N, W, bias, out, aux, epi)
+    res = {(n, i): [] for n in shapes for i in impls}
+    ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+    for _ in range(5):
+        for name, (N, W, bias, out, aux, epi) in bufs.items():
+            for impl in impls:
+                K.set_gemm_impl(impl)
+                fn = lambda: K.gemm(K.FWD, epi, M, N, C, x, C, W, C, out, N, bias=bias, aux=aux,  # noqa: E731
+                                    ldaux=N if aux is not None else 0, p_drop=0.1 if aux is not None else 0.0, seed=5)
+                fn()
+                s, e = ev(), ev()
+                s.record()
+                for _r in range(10):
+                    fn()
+                e.record()
+                torch.cuda.synchronize()
+                res[(name, impl)].append(s.elapsed_time(e) / 10)
+    K.set_gemm_impl(0)
+    for name, (N, *_r) in bufs.items():
+        line = f"{name:20s}"
+        for impl in impls:
+            t = sorted(res[(name, impl)])[2]
+            line += f"  impl{impl}: {t * 1e3:8.1f} us {2 * M * N * C / t / 1e9:7.0f} TF"
+        print(line, flush=True)
+
+
+if __name__ == "__main__":
+    main()
