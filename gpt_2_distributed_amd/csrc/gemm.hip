@@ -210,8 +210,8 @@ int launch(const GemmParams& P, int splits, hipStream_t s) {
 }  // namespace
 
 // 0 auto (ping-pong 256x256, persistent for short K), 1 force 128x128, 2 force the 2-stage 256x256, 3..5
-// ping-pong with half-tile map 1..3, 6 ping-pong without the persistent schedule (A/B experiments,
-// tools/gemm_probe.py)
+// ping-pong with half-tile map 1..3, 6 ping-pong without the persistent schedule, 7 persistent at any K
+// (A/B experiments, tools/gemm_probe.py, tools/gemm_ab.py)
 static int g_gemm_impl = 0;
 GPT2MI_EXPORT void gpt2mi_set_gemm_impl(int impl) { g_gemm_impl = impl; }
 
@@ -253,7 +253,7 @@ GPT2MI_EXPORT int gpt2mi_gemm(int layout, int epilogue, int M, int N, int K, con
   const bool big_ok = splits == 1 && N % 256 == 0 && epilogue != EPI_ATOMIC && (layout <= 1 || M % 256 == 0);
   if (big_ok && (g_gemm_impl == 0 || g_gemm_impl >= 3)) {
     // impl 6: the ping-pong kernel without its persistent schedule (A/B)
-    const int map = g_gemm_impl == 6 ? -1 : g_gemm_impl >= 3 ? g_gemm_impl - 2 : 0;
+    const int map = g_gemm_impl == 6 ? -1 : g_gemm_impl == 7 ? 7 : g_gemm_impl >= 3 ? g_gemm_impl - 2 : 0;
     const int rc = gpt2mi::gemm_pp_dispatch(layout, epilogue, P, s, 1, map);
     if (rc >= 0) return rc;  // the ping-pong kernel fuses dbias
   }

@@ -572,14 +572,15 @@ int gemm_pp_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t 
     }
   }
   // short-K forward-layout shapes with no epilogue operand loads: the persistent schedule (map < 0 forces
-  // the one-tile-per-block kernel, tools/gemm_probe.py A/B)
+  // the one-tile-per-block kernel, map 7 the persistent one at any K: tools/gemm_ab.py)
   const int ntiles = ((P.M + BM - 1) / BM) * (P.N / BN);
-  if (layout == 0 && map == 0 && P.K <= 1024 && ntiles >= 2 * num_cus() && P.dbias == nullptr &&
+  if (layout == 0 && (map == 0 || map == 7) && (P.K <= 1024 || map == 7) && ntiles >= 2 * num_cus() &&
+      P.dbias == nullptr &&
       (epilogue == EPI_BF16 || epilogue == EPI_GELU) && P.M % BM == 0 && (size_t)P.M * P.lda * 2 < (1ull << 31) &&
       (size_t)P.N * P.ldb * 2 < (1ull << 31)) {
     return epilogue == EPI_BF16 ? launch_persistent<EPI_BF16>(P, s) : launch_persistent<EPI_GELU>(P, s);
   }
-  if (map < 0) map = 0;
+  if (map < 0 || map == 7) map = 0;
   switch (layout * 16 + epilogue) {
     case 0 * 16 + EPI_BF16: return launch<false, false, EPI_BF16>(P, s, 1);
     case 0 * 16 + EPI_F32: return launch<false, false, EPI_F32>(P, s, 1);

@@ -19,26 +19,36 @@ def main():
     M, C, Vp = 65536, 768, 50432
     g = torch.Generator(device=dev).manual_seed(0)
     rnd = lambda *s, sc=1.0: (torch.randn(*s, device=dev, generator=g) * sc).to(torch.bfloat16)  # noqa: E731
-    x = rnd(M, C)
+    # (N, bias?, epilogue, K): forward shapes (K = C) and the dgrads that run in the forward layout against W^T
     shapes = {
-        "lm_head fwd": (Vp, None, K.EPI_BF16),
-        "qkv fwd +bias": (3 * C, True, K.EPI_BF16),
-        "fc1 fwd gelu+drop": (4 * C, True, K.EPI_GELU),
+        "lm_head fwd": (Vp, None, K.EPI_BF16, C),
+        "qkv fwd +bias": (3 * C, True, K.EPI_BF16, C),
+        "fc1 fwd gelu+drop": (4 * C, True, K.EPI_GELU, C),
+        "proj dgrad": (C, None, K.EPI_BF16, C),
+        "qkv dgrad": (C, None, K.EPI_BF16, 3 * C),
+        "fc1 dgrad": (C, None, K.EPI_BF16, 4 * C),
+        "lm_head dgrad": (C, None, K.EPI_BF16, Vp),
     }
+    if os.environ.get("GEMM_AB_SHAPES"):
+        shapes = {k: v for k, v in shapes.items() if any(s in k for s in os.environ["GEMM_AB_SHAPES"].split(","))}
     bufs = {}
-    for name, (N, has_bias, epi) in shapes.items():
-        W = rnd(N, C, sc=0.05)
+    xs = {}
+    for name, (N, has_bias, epi, Kd) in shapes.items():
+        if Kd not in xs:
+            xs[Kd] = rnd(M, Kd)
+        W = rnd(N, Kd, sc=0.05)
         bias = torch.randn(N, device=dev) if has_bias else None
         out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
         aux = torch.empty(M, N, dtype=torch.bfloat16, device=dev) if epi == K.EPI_GELU else None
-        bufs[name] = (N, W, bias, out, aux, epi)
+        bufs[name] = (N, W, bias, out, aux, epi, Kd)
     res = {(n, i): [] for n in shapes for i in impls}
     ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
     for _ in range(5):
-        for name, (N, W, bias, out, aux, epi) in bufs.items():
+        for name, (N, W, bias, out, aux, epi, Kd) in bufs.items():
             for impl in impls:
                 K.set_gemm_impl(impl)
-                fn = lambda: K.gemm(K.FWD, epi, M, N, C, x, C, W, C, out, N, bias=bias, aux=aux,  # noqa: E731
+                xa = xs[Kd]
+                fn = lambda: K.gemm(K.FWD, epi, M, N, Kd, xa, Kd, W, Kd, out, N, bias=bias, aux=aux,  # noqa: E731
                                     ldaux=N if aux is not None else 0, p_drop=0.1 if aux is not None else 0.0, seed=5)
                 fn()
                 s, e = ev(), ev()
@@ -50,10 +60,11 @@ def main():
                 res[(name, impl)].append(s.elapsed_time(e) / 10)
     K.set_gemm_impl(0)
     for name, (N, *_r) in bufs.items():
+        Kd = bufs[name][-1]
         line = f"{name:20s}"
         for impl in impls:
             t = sorted(res[(name, impl)])[2]
-            line += f"  impl{impl}: {t * 1e3:8.1f} us {2 * M * N * C / t / 1e9:7.0f} TF"
+            line += f"  impl{impl}: {t * 1e3:8.1f} us {2 * M * N * Kd / t / 1e9:7.0f} TF"
         print(line, flush=True)
 
 
