@@ -56,6 +56,29 @@ __device__ __forceinline__ void dma_tile(const bf16* __restrict__ src, int ld, i
   }
 }
 
+// The m-contiguous operand's K-tile by BUFFER LDS-DMA (WG_BUFDMA): the descriptor is rebased on the K-tile
+// (k0 * ld elements, scalar registers), so the per-lane part of the source offset — k-row parity (l >> 5)
+// and the swizzled 16-B chunk — takes two VGPRs for every K-tile (instruction t and t + 2 share a
+// swizzle) and the k-row / column block is a wave-uniform soffset: no 64-bit address math per DMA.
+#ifndef WG_BUFDMA
+#define WG_BUFDMA 1
+#endif
+__device__ __forceinline__ uint32_t mc_lane_off(int ld, int wid, int par, int lane) {
+  const int k = 8 * (wid & 1) + 2 * par + (lane >> 5);  // k-row mod 16 of instruction t = par (mod 2)
+  return (uint32_t)(((lane >> 5) * ld + 8 * ((lane & 31) ^ mc_swz(k))) * (int)sizeof(bf16));
+}
+__device__ __forceinline__ void dma_tile_mc_buf(const bf16* __restrict__ src, int ld, int row0, int k0,
+                                                const uint32_t (&loff)[2], char* tile, int wid) {
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(src + (size_t)k0 * ld), 0, 0x7fffffff, 0x00020000);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int ins = wid * 4 + t;
+    const int soff = ((2 * ins) * ld + row0) * (int)sizeof(bf16);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(tile + ins * 1024), 16, loff[t & 1], soff, 0, 0);
+  }
+}
+
 __device__ __forceinline__ bf16x8 frag_kc(const char* base, int row, int chunk) {
   return *reinterpret_cast<const bf16x8*>(base + kc_off(row, chunk));
 }
@@ -101,18 +124,30 @@ __global__ __launch_bounds__(kThreads, 1) void gemm256_kernel(GemmParams P) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  dma_tile<A_T>(P.A, P.lda, m0, kbeg, P.M - 1, smem, wid, lane);
-  dma_tile<B_T>(P.B, P.ldb, n0, kbeg, P.N - 1, smem + kOpBytes, wid, lane);
+  constexpr bool kBufDma = WG_BUFDMA && A_T && B_T;  // the weight-gradient instantiation
+  [[maybe_unused]] uint32_t loff_a[2] = {0, 0}, loff_b[2] = {0, 0};
+  if constexpr (kBufDma) {
+    loff_a[0] = mc_lane_off(P.lda, wid, 0, lane);
+    loff_a[1] = mc_lane_off(P.lda, wid, 1, lane);
+    loff_b[0] = mc_lane_off(P.ldb, wid, 0, lane);
+    loff_b[1] = mc_lane_off(P.ldb, wid, 1, lane);
+  }
+  auto stage = [&](int k0, char* dst) {
+    if constexpr (kBufDma) {
+      dma_tile_mc_buf(P.A, P.lda, m0, k0, loff_a, dst, wid);
+      dma_tile_mc_buf(P.B, P.ldb, n0, k0, loff_b, dst + kOpBytes, wid);
+    } else {
+      dma_tile<A_T>(P.A, P.lda, m0, k0, P.M - 1, dst, wid, lane);
+      dma_tile<B_T>(P.B, P.ldb, n0, k0, P.N - 1, dst + kOpBytes, wid, lane);
+    }
+  };
+  stage(kbeg, smem);
   asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
 
   for (int kt = 0; kt < nk; ++kt) {
     const char* As = smem + (kt & 1) * kStageBytes;
     const char* Bs = As + kOpBytes;
-    if (kt + 1 < nk) {
-      char* nxt = smem + ((kt + 1) & 1) * kStageBytes;
-      dma_tile<A_T>(P.A, P.lda, m0, kbeg + (kt + 1) * BK, P.M - 1, nxt, wid, lane);
-      dma_tile<B_T>(P.B, P.ldb, n0, kbeg + (kt + 1) * BK, P.N - 1, nxt + kOpBytes, wid, lane);
-    }
+    if (kt + 1 < nk) stage(kbeg + (kt + 1) * BK, smem + ((kt + 1) & 1) * kStageBytes);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       bf16x8 bf[4];

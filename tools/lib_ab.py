@@ -1,0 +1,83 @@
+#!/usr/bin/env python
+"""A/B of library builds (same C ABI) on the GPT-2 124M weight-gradient shapes (K = 65536 tokens): every
+library in argv is loaded side by side with ctypes, outputs are compared bitwise against the first, and
+the wgrad GEMM (gpt2mi_gemm_wgrad, the split-K choice of _lib.wgrad_splits) is timed in interleaved rounds.
+
+    python tools/lib_ab.py libA.so libB.so ...
+"""
+import ctypes
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from gpt_2_distributed_amd import _lib as K  # noqa: E402
+
+dev = "cuda"
+
+
+def bind(path):
+    lib = ctypes.CDLL(path)
+    for name, args in K._SIGS.items():
+        if hasattr(lib, name):
+            fn = getattr(lib, name)
+            fn.argtypes = args
+            fn.restype = K._RESTYPES.get(name, ctypes.c_int)
+    return lib
+
+
+def main():
+    libs = [bind(p) for p in sys.argv[1:]]
+    Mt, C, Vp = 65536, 768, 50432
+    shapes = {"lm_head wgrad": (Vp, C), "qkv wgrad": (3 * C, C), "fc1 wgrad": (4 * C, C), "fc2 wgrad": (C, 4 * C),
+              "proj wgrad": (C, C)}
+    g = torch.Generator(device=dev).manual_seed(0)
+    st = torch.cuda.current_stream().cuda_stream
+    data = {}
+    for name, (m, n) in shapes.items():
+        A = (torch.randn(Mt, m, device=dev, generator=g) * 0.1).to(torch.bfloat16)
+        B = (torch.randn(Mt, n, device=dev, generator=g)).to(torch.bfloat16)
+        sp = K.wgrad_splits(m, n, Mt)
+        ws = torch.empty(max(sp * m * n, 4), device=dev)
+        data[name] = (m, n, A, B, sp, ws)
+    outs = {}
+    for i, lib in enumerate(libs):
+        for name, (m, n, A, B, sp, ws) in data.items():
+            Cm = torch.zeros(m, n, device=dev)
+            rc = lib.gpt2mi_gemm_wgrad(m, n, Mt, A.data_ptr(), m, B.data_ptr(), n, Cm.data_ptr(), n, 0, 1.0, None,
+                                       ws.data_ptr(), ws.numel(), sp, st)
+            assert rc == 0, (i, name, rc)
+            outs[(i, name)] = Cm
+    torch.cuda.synchronize()
+    for name in shapes:
+        for i in range(1, len(libs)):
+            if not torch.equal(outs[(0, name)], outs[(i, name)]):
+                d = (outs[(0, name)] - outs[(i, name)]).abs().max().item()
+                print(f"MISMATCH lib{i} {name}: max diff {d}")
+    times = {k: [] for k in outs}
+    ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+    for _ in range(5):
+        for name, (m, n, A, B, sp, ws) in data.items():
+            for i, lib in enumerate(libs):
+                Cm = outs[(i, name)]
+                fn = lambda: lib.gpt2mi_gemm_wgrad(m, n, Mt, A.data_ptr(), m, B.data_ptr(), n, Cm.data_ptr(), n, 1,  # noqa
+                                                   1.0, None, ws.data_ptr(), ws.numel(), sp, st)
+                fn()
+                s, e = ev(), ev()
+                s.record()
+                for _r in range(5):
+                    fn()
+                e.record()
+                torch.cuda.synchronize()
+                times[(i, name)].append(s.elapsed_time(e) / 5)
+    for name, (m, n, *_r) in data.items():
+        line = f"{name:14s}"
+        for i in range(len(libs)):
+            t = sorted(times[(i, name)])[2]
+            line += f"  lib{i}: {t * 1e3:8.1f} us {2 * m * n * Mt / t / 1e9:6.0f} TF"
+        print(line, flush=True)
+
+
+if __name__ == "__main__":
+    main()
