@@ -76,9 +76,11 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    from gpt_2_distributed_amd.parallel import init_distributed, local_device_index
+    from gpt_2_distributed_amd.parallel import init_distributed, local_device_index, use_collectives
     local_rank = local_device_index()
-    if world > 1:
+    # a torchrun launch of one rank with GPT2MI_FORCE_COLLECTIVES=1 runs the wrapper and its RCCL calls too
+    wrapped = world > 1 or ("WORLD_SIZE" in os.environ and use_collectives(world))
+    if wrapped:
         init_distributed()
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
@@ -88,7 +90,7 @@ def main():
                      attn_pdrop=args.dropout)
     model = GPT2(cfg).to(dev)
     model.train()
-    if world > 1:
+    if wrapped:
         from gpt_2_distributed_amd.parallel import DistributedDataParallel, ShardedDataParallel
         wrap = ShardedDataParallel if args.parallel == "fsdp" else DistributedDataParallel
         ddp = wrap(model, bucket_mb=args.bucket_mb)
@@ -124,23 +126,23 @@ def main():
     for i in range(args.warmup):
         loss = step(i)
     torch.cuda.synchronize()
-    if world > 1:
+    if wrapped:
         dist.barrier()
     probes = ["lm_head_fwd", "lm_head_dgrad", "lm_head_wgrad", "fc1_fwd", "attn_fwd"]
     eng.probes = {p: [] for p in probes}
     torch.cuda.synchronize()
-    if world > 1:
+    if wrapped:
         dist.barrier()
     t0 = time.perf_counter()
     for i in range(args.steps):
         loss = step(i)
     torch.cuda.synchronize()
-    if world > 1:
+    if wrapped:
         dist.barrier()
     dt = time.perf_counter() - t0
     eng.probes, armed = {}, eng.probes
     dt_t = torch.tensor([dt], device=dev)
-    if world > 1:
+    if wrapped:
         dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
     dt = float(dt_t.item())
     final_loss = float(loss.item())
@@ -194,10 +196,10 @@ def main():
         "config": {"workload": f"GPT-2 {args.model} training step: fwd+loss+bwd+AdamW"
                                + ({"ddp": " + bucketed grad all-reduce in the backward",
                                    "fsdp": " + per-block FSDP all-gather / reduce-scatter"}[args.parallel]
-                                  if world > 1 else "")
+                                  if wrapped else "")
                                + f", dropout {args.dropout}" + (f", {GA} accumulated micro-batches" if GA > 1 else ""),
                    "model": f"GPT-2 {args.model}", "global_batch": B * world * GA, "seq_len": T,
-                   "parallelism": f"{'fsdp' if args.parallel == 'fsdp' and world > 1 else 'dp'}{world}"},
+                   "parallelism": f"{'fsdp' if args.parallel == 'fsdp' and wrapped else 'dp'}{world}"},
         "mfu": round(tok_s * fpt / (world * PEAK_BF16_TFLOPS * 1e12), 4),
         "flop_per_token": fpt,
         "final_loss": round(final_loss * GA, 4),
@@ -212,7 +214,7 @@ def main():
             out["cpu_baseline"] = {"error": repr(e)}
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if wrapped:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -91,7 +91,7 @@ class ShardedAdamW(_FlatAdamW):
         f = self.fsdp
         self._run(f.flat_param.detach(), f.grad_shard, f.shard_bf16)
         f.mark_params_updated(bf16_fresh=True)
-        if f.world > 1:  # the clip_grad_norm_(inf) value of the full model: sum of squares over shards
+        if f.coll:  # the clip_grad_norm_(inf) value of the full model: sum of squares over shards
             n2 = self.grad_norm.square()
             dist.all_reduce(n2)
             self.grad_norm.copy_(n2.sqrt())

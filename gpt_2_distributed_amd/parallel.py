@@ -70,6 +70,13 @@ def init_distributed() -> None:
         torch.cuda.set_device(local_device_index())
 
 
+def use_collectives(world: int) -> bool:
+    """Collectives run when world > 1. GPT2MI_FORCE_COLLECTIVES=1 also runs them in a world of one: a
+    one-GPU box then drives the real RCCL calls (async all-reduce from the backward, all-gather /
+    reduce-scatter on the wrapper's buffers) that the multi-GPU node runs."""
+    return world > 1 or os.environ.get("GPT2MI_FORCE_COLLECTIVES") == "1"
+
+
 def is_primary() -> bool:
     return dist.get_rank() == 0 if dist.is_initialized() else True
 
@@ -161,6 +168,7 @@ class _DPHooks(GradHooks):
     def __init__(self, engine, world: int):
         self.engine = engine
         self.world = world
+        self.coll = use_collectives(world)
         self.sync = True
 
     def begin_backward(self) -> float:
@@ -178,11 +186,11 @@ class _DDPHooks(_DPHooks):
         self.reducer = reducer
 
     def ready(self, name):
-        if self.sync and self.world > 1:
+        if self.sync and self.coll:
             self.reducer.mark_ready(name)
 
     def end_backward(self):
-        if self.sync and self.world > 1:
+        if self.sync and self.coll:
             self.reducer.finish()
 
 
@@ -195,7 +203,7 @@ class DistributedDataParallel(nn.Module):
         eng = module.engine()
         self.engine = eng
         world = dist.get_world_size()
-        if broadcast and world > 1:
+        if broadcast and use_collectives(world):
             dist.broadcast(module.arena, src=0)
             eng.refresh_shadow()
         units = unit_ranges(module.layout, module.config.n_layer)
@@ -282,7 +290,8 @@ class FullyShardedDataParallel(nn.Module):
         self.rank = dist.get_rank()
         self.prefetch = prefetch
         W, r = self.world, self.rank
-        if W > 1:
+        self.coll = use_collectives(W)
+        if self.coll:
             dist.broadcast(module.arena, src=0)
         self.units = unit_ranges(module.layout, module.config.n_layer)
         self.plans, self.shard_total = plan_shards(self.units, W)
@@ -363,7 +372,7 @@ class FullyShardedDataParallel(nn.Module):
         else:
             src = self.flat_param.detach()[p.soff:p.soff + p.per]
         out = self._buf("ag", unit, dtype, p.per * self.world)
-        if self.world == 1:
+        if not self.coll:
             out.copy_(src)
             work = None
         else:
@@ -407,7 +416,7 @@ class FullyShardedDataParallel(nn.Module):
         inp = self._buf("rs_in", unit, dtype, p.per * self.world)
         K.fsdp_pack(eng.grad[p.lo:p.hi], inp, p.n, p.per * self.world)
         out = self._buf("rs_out", unit, dtype, p.per)
-        if self.world == 1:
+        if not self.coll:
             out.copy_(inp)
             work = None
         else:
@@ -466,7 +475,7 @@ class FullyShardedDataParallel(nn.Module):
         for p in self.plans:
             src = self.flat_param.detach()[p.soff:p.soff + p.per]
             out = torch.empty(p.per * self.world, dtype=torch.float32, device=arena.device)
-            if self.world == 1:
+            if not self.coll:
                 out.copy_(src)
             else:
                 dist.all_gather_into_tensor(out, src)

@@ -39,7 +39,8 @@ init_distributed()
 r, w = dist.get_rank(), dist.get_world_size()
 G = json.load(open(os.environ["GOLDEN"]))
 cfg = GPT2Config(**G["config"])
-S, GA, P = G["steps"], G["grad_accum"], G["per_rank"]
+S, GA = G["steps"], G["grad_accum"]
+P = G["world"] * G["per_rank"] // w  # the golden's rows split over this launch's ranks
 toks = torch.randint(0, 509, (S, GA, w * P, 65), generator=torch.Generator().manual_seed(5))
 
 def build(mode, opt_kind):
@@ -112,20 +113,38 @@ VARIANTS = ["ddp/fused/fp32", "ddp/fused/bf16", "ddp/torch/fp32", "ddp/nosync/fp
             "fsdp/fused/bf16", "fsdp/ckpt/bf16", "ddp/ckpt/fp32"]
 
 
+def _launch(tmp, nproc, variants, port, **env_extra):
+    script = tmp / "w.py"
+    script.write_text(WORKER)
+    env = dict(os.environ, REPO=REPO, GOLDEN=os.path.join(GOLDEN, "ddp_golden.json"), VARIANTS=",".join(variants),
+               CKPT_DIR=str(tmp / "ckpt"), **env_extra)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", str(script)]
+    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=400)
+    assert out.returncode == 0, out.stderr[-4000:]
+    return json.loads([l for l in out.stdout.splitlines() if l.startswith("RESULT")][0][7:])
+
+
 @pytest.fixture(scope="module")
 def results(tmp_path_factory):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    tmp = tmp_path_factory.mktemp("ddp")
-    script = tmp / "w.py"
-    script.write_text(WORKER)
-    env = dict(os.environ, REPO=REPO, GOLDEN=os.path.join(GOLDEN, "ddp_golden.json"), VARIANTS=",".join(VARIANTS),
-               CKPT_DIR=str(tmp / "ckpt"), GPT2MI_SINGLE_DEVICE="1", GPT2MI_DIST_BACKEND="gloo")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", "--master-port=29555", str(script)]
-    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=400)
-    assert out.returncode == 0, out.stderr[-4000:]
-    return json.loads([l for l in out.stdout.splitlines() if l.startswith("RESULT")][0][7:])
+    return _launch(tmp_path_factory.mktemp("ddp"), 2, VARIANTS, 29555, GPT2MI_SINGLE_DEVICE="1",
+                   GPT2MI_DIST_BACKEND="gloo")
+
+
+RCCL_VARIANTS = ["ddp/fused/fp32", "ddp/fused/bf16", "ddp/torch/fp32", "fsdp/fused/fp32", "fsdp/fused/bf16"]
+
+
+@pytest.fixture(scope="module")
+def rccl_results(tmp_path_factory):
+    """One rank on the backend the multi-GPU node uses ("nccl" = RCCL), with GPT2MI_FORCE_COLLECTIVES=1 so
+    the bucketed all-reduce from inside the backward, the FSDP all-gathers / reduce-scatters and the grad
+    norm all-reduce really run through RCCL (a world of one: each collective is RCCL's copy)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return _launch(tmp_path_factory.mktemp("rccl"), 1, RCCL_VARIANTS, 29556, GPT2MI_DIST_BACKEND="nccl",
+                   GPT2MI_FORCE_COLLECTIVES="1")
 
 
 GOLD = json.load(open(os.path.join(GOLDEN, "ddp_golden.json")))
@@ -135,10 +154,8 @@ GOLD = json.load(open(os.path.join(GOLDEN, "ddp_golden.json")))
 TOL = {"fp32": (1e-4, 1e-3, 1e-4), "bf16": (2e-2, 5e-2, 3e-2)}
 
 
-@pytest.mark.parametrize("variant", [v for v in VARIANTS if "ckpt" not in v])
-def test_two_ranks_vs_reference_concatenated_batch(results, variant):
+def _check_vs_golden(r, variant):
     t_loss, t_norm, t_par = TOL[variant.split("/")[2]]
-    r = results[variant]
     rl = np.abs(np.array(r["losses"]) - GOLD["losses"]) / np.array(GOLD["losses"])
     assert rl.max() < t_loss, (variant, r["losses"], GOLD["losses"])
     rn = np.abs(np.array(r["norms"]) - GOLD["grad_norms"]) / np.array(GOLD["grad_norms"])
@@ -155,6 +172,33 @@ def test_two_ranks_vs_reference_concatenated_batch(results, variant):
         if fp32:
             np.testing.assert_allclose(head, g["head"], rtol=t_par, atol=1e-2 * GOLD["lr"], err_msg=f"{variant} {n}")
     assert abs(tot - tot_ref) <= 1e-2 * tot_ref, variant
+
+
+@pytest.mark.parametrize("variant", [v for v in VARIANTS if "ckpt" not in v])
+def test_two_ranks_vs_reference_concatenated_batch(results, variant):
+    _check_vs_golden(results[variant], variant)
+
+
+@pytest.mark.parametrize("variant", RCCL_VARIANTS)
+def test_rccl_collectives_vs_reference(rccl_results, variant):
+    _check_vs_golden(rccl_results[variant], variant)
+
+
+@pytest.mark.parametrize("parallel", ["ddp", "fsdp"])
+def test_bench_wrapped_rccl_one_rank(parallel):
+    """bench.py's multi-GPU path (torchrun, RCCL, the wrapper, barrier + MAX-over-ranks timing) on one rank
+    with the collectives forced on: one JSON line, finite loss."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    env = dict(os.environ, GPT2MI_FORCE_COLLECTIVES="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr=127.0.0.1", "--master-port=29557", os.path.join(REPO, "bench.py"), "--gpus", "1",
+           "--steps", "2", "--warmup", "1", "--batch", "4", "--parallel", parallel, "--no-cpu-baseline"]
+    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=REPO)
+    assert out.returncode == 0, out.stderr[-4000:]
+    line = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["config"]["parallelism"] == ("fsdp1" if parallel == "fsdp" else "dp1")
+    assert np.isfinite(line["final_loss"]) and line["value"] > 0
 
 
 @pytest.mark.parametrize("variant", ["fsdp/ckpt/bf16", "ddp/ckpt/fp32"])
