@@ -47,7 +47,6 @@ constexpr int kBuf = 4 * kHalf;      // A_0, A_1, B_0, B_1
 constexpr int kLds = 2 * kBuf;       // 128 KiB
 constexpr int SA0 = 0, SA1 = kHalf, SB0 = 2 * kHalf, SB1 = 3 * kHalf;
 
-typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 __device__ __forceinline__ int mc_swz(int k) { return 2 * ((k & 3) | (((k >> 3) & 1) << 2)); }
@@ -82,7 +81,7 @@ __device__ __forceinline__ void dma_half(const bf16* __restrict__ src, int ld, i
       const int c = (lane & 15) ^ mc_swz(k);
       g = src + (size_t)(k0 + k) * ld + base + half_map<IL, IS_A>(8 * c, h);
     }
-    __builtin_amdgcn_global_load_lds((const void*)g, (lds_void*)(slot + ins * 1024), 16, 0, 0);
+    lds_dma16(g, slot + ins * 1024);
   }
 }
 
@@ -93,13 +92,12 @@ __device__ __forceinline__ void dma_half(const bf16* __restrict__ src, int ld, i
 __device__ __forceinline__ uint32_t kc_lane_off(int ld, int lane) {
   return (uint32_t)(((lane >> 3) * ld + 8 * ((lane & 7) ^ (lane >> 3))) * (int)sizeof(bf16));
 }
-__device__ __forceinline__ void dma_half_buf(__amdgpu_buffer_rsrc_t rs, int ld, int row0, int k0, uint32_t loff,
-                                             char* slot, int wid) {
+__device__ __forceinline__ void dma_half_buf(u32x4 rs, int ld, int row0, int k0, uint32_t loff, char* slot, int wid) {
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     const int ins = wid * 2 + t;
     const int soff = ((row0 + 8 * ins) * ld + k0) * (int)sizeof(bf16);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(slot + ins * 1024), 16, loff, soff, 0, 0);
+    lds_dma16_buf(rs, loff, soff, slot + ins * 1024);
   }
 }
 
@@ -249,11 +247,11 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   auto kofs = [&](int t) { return kbeg + t * BK; };
   // PERSIST (k-contiguous A and B): buffer DMA, 2 lane-offset VGPRs for every tile instead of per-tile
   // 64-bit row pointers (the persistent loop keeps its registers under the 256 of 2 waves/SIMD)
-  [[maybe_unused]] __amdgpu_buffer_rsrc_t rs_a, rs_b;
+  [[maybe_unused]] u32x4 rs_a, rs_b;
   [[maybe_unused]] uint32_t loff_a = 0, loff_b = 0;
   if constexpr (PERSIST) {
-    rs_a = __builtin_amdgcn_make_buffer_rsrc((void*)P.A, 0, 0x7fffffff, 0x00020000);
-    rs_b = __builtin_amdgcn_make_buffer_rsrc((void*)P.B, 0, 0x7fffffff, 0x00020000);
+    rs_a = buf_desc(P.A);
+    rs_b = buf_desc(P.B);
     loff_a = kc_lane_off(P.lda, lane);
     loff_b = kc_lane_off(P.ldb, lane);
   }
@@ -559,7 +557,12 @@ int gemm_pp_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t 
   if (P.N % BN != 0 || P.k_per_split % (2 * BK) != 0 || P.K % (2 * BK) != 0) return -1;
   // wgrad (both operands m-contiguous) runs on the 2-stage gemm256 kernel: this one measured
   // 698-721 TF vs 765 TF on the lm_head wgrad, 756 vs 852 on qkv (tools/gemm_probe.py, every map)
-  if (layout == 2) return -1;
+  // (map 8: run it anyway, A/B in tools/lib_ab.py)
+  if (layout == 2) {
+    if (map != 8) return -1;
+    return epilogue == EPI_SLAB ? launch<true, true, EPI_SLAB>(P, s, splits)
+                                : epilogue == EPI_F32 ? launch<true, true, EPI_F32>(P, s, 1) : -1;
+  }
   if (map > 0 && epilogue == EPI_BF16 && layout <= 1) {  // half-tile map experiments (tools/gemm_probe.py)
     if (layout == 0) {
       if (map == 1) return launch<false, false, EPI_BF16, 1>(P, s, 1);

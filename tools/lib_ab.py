@@ -17,8 +17,14 @@ from gpt_2_distributed_amd import _lib as K  # noqa: E402
 dev = "cuda"
 
 
-def bind(path):
-    lib = ctypes.CDLL(path)
+def bind(path, _n=[0]):
+    # a private copy per argument, so the same library can be listed twice with different settings
+    import shutil
+    import tempfile
+    _n[0] += 1
+    cp = os.path.join(tempfile.mkdtemp(), f"lib{_n[0]}.so")
+    shutil.copy(path, cp)
+    lib = ctypes.CDLL(cp)
     for name, args in K._SIGS.items():
         if hasattr(lib, name):
             fn = getattr(lib, name)
@@ -29,6 +35,10 @@ def bind(path):
 
 def main():
     libs = [bind(p) for p in sys.argv[1:]]
+    # LIB_AB_IMPLS=0,8: gpt2mi_set_gemm_impl per library (the same .so may be listed twice)
+    impls = [int(v) for v in os.environ.get("LIB_AB_IMPLS", "").split(",") if v]
+    for lib, impl in zip(libs, impls):
+        lib.gpt2mi_set_gemm_impl(impl)
     Mt, C, Vp = 65536, 768, 50432
     shapes = {"lm_head wgrad": (Vp, C), "qkv wgrad": (3 * C, C), "fc1 wgrad": (4 * C, C), "fc2 wgrad": (C, 4 * C),
               "proj wgrad": (C, C)}
@@ -41,6 +51,8 @@ def main():
         sp = K.wgrad_splits(m, n, Mt)
         ws = torch.empty(max(sp * m * n, 4), device=dev)
         data[name] = (m, n, A, B, sp, ws)
+    if os.environ.get("LIB_AB_OP") == "gemm":
+        return gemm_mode(libs, g, st)
     outs = {}
     for i, lib in enumerate(libs):
         for name, (m, n, A, B, sp, ws) in data.items():
@@ -76,6 +88,43 @@ def main():
         for i in range(len(libs)):
             t = sorted(times[(i, name)])[2]
             line += f"  lib{i}: {t * 1e3:8.1f} us {2 * m * n * Mt / t / 1e9:6.0f} TF"
+        print(line, flush=True)
+
+
+def gemm_mode(libs, g, st):
+    """LIB_AB_OP=gemm: forward / dgrad layouts (gpt2mi_gemm, BF16 epilogue) on the lm_head and K=768 shapes."""
+    Mt, C, Vp = 65536, 768, 50432
+    # name: (layout, N, K)
+    shapes = {"lm_head fwd": (0, Vp, C), "lm_head dgrad": (1, C, Vp), "qkv fwd": (0, 3 * C, C), "fc1 dgrad": (1, C, 4 * C)}
+    data = {}
+    for name, (lay, n, k) in shapes.items():
+        A = (torch.randn(Mt, k, device=dev, generator=g) * 0.1).to(torch.bfloat16)
+        B = (torch.randn(n, k, device=dev, generator=g) if lay == 0 else
+             torch.randn(k, n, device=dev, generator=g)).to(torch.bfloat16)
+        out = torch.empty(Mt, n, dtype=torch.bfloat16, device=dev)
+        data[name] = (lay, n, k, A, B, out)
+    times = {(i, n): [] for i in range(len(libs)) for n in shapes}
+    ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+    for _ in range(5):
+        for name, (lay, n, k, A, B, out) in data.items():
+            ldb = k if lay == 0 else n
+            for i, lib in enumerate(libs):
+                fn = lambda: lib.gpt2mi_gemm(lay, 0, Mt, n, k, A.data_ptr(), k, B.data_ptr(), ldb,  # noqa: E731
+                                             out.data_ptr(), n, None, None, None, 0, 1.0, None, 0, 1, 0.0, 0,
+                                             None, st)
+                assert fn() == 0
+                s, e = ev(), ev()
+                s.record()
+                for _r in range(5):
+                    fn()
+                e.record()
+                torch.cuda.synchronize()
+                times[(i, name)].append(s.elapsed_time(e) / 5)
+    for name, (lay, n, k, *_r) in data.items():
+        line = f"{name:14s}"
+        for i in range(len(libs)):
+            t = sorted(times[(i, name)])[2]
+            line += f"  lib{i}: {t * 1e3:8.1f} us {2 * n * k * Mt / t / 1e9:6.0f} TF"
         print(line, flush=True)
 
 
