@@ -31,37 +31,6 @@ struct GemmParams {
   float inv_keep;
 };
 
-// ---- LDS-DMA issued by inline asm --------------------------------------------------------------------------
-// hipcc's waitcnt pass cannot tell which LDS bytes an LDS-DMA (global_load_lds / buffer_load ... lds) writes, so
-// after one it drains ALL vector memory (s_waitcnt vmcnt(0)) before the next LDS read of any address: in a
-// multi-stage GEMM that waits for the DMAs just issued for a LATER K-tile and serialises the operand feed with
-// the MFMAs. Issued from asm the DMAs are invisible to that pass; the GEMM kernels retire them with their own
-// counted s_waitcnt vmcnt(N) + s_barrier (RAW) and restage a slot only after a barrier that follows its last
-// read (WAR). The compiler's own waits for its ordinary loads stay correct: vector memory loads retire in issue
-// order, so extra (asm) loads in flight only make a counted wait wait longer.
-// M0 = the LDS destination of the wave's 64 x 16 B (lane-linear; an operand bound to m0). The hazard recognizer
-// does not look inside asm: s_nop 4 covers the M0-write -> LDS-DMA (1) and VALU-SGPR-write -> VMEM-read (5) wait
-// states of the SGPR operands (descriptor, soffset, M0).
-typedef __attribute__((address_space(3))) void lds_void;
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {  // generic pointer into LDS -> LDS byte address
-  return (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const lds_void*)p);
-}
-__device__ __forceinline__ void lds_dma16(const void* gptr, const void* lds_dst) {
-  const uint32_t m0 = lds_addr(lds_dst);
-  asm volatile("s_nop 4\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gptr), "{m0}"(m0) : "memory");
-}
-// raw buffer descriptor over [base, base + 2 GiB) (the same words __builtin_amdgcn_make_buffer_rsrc forms on gfx950)
-__device__ __forceinline__ u32x4 buf_desc(const void* base) {
-  const uint64_t a = (uint64_t)(uintptr_t)base;
-  return u32x4{(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)a),
-               (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32) & 0xffffu), 0x7fffffffu, 0x00020000u};
-}
-__device__ __forceinline__ void lds_dma16_buf(u32x4 desc, uint32_t voff, int soff, const void* lds_dst) {
-  const uint32_t m0 = lds_addr(lds_dst);
-  asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(voff), "s"(desc), "s"(soff), "{m0}"(m0)
-               : "memory");
-}
-
 // keep mask of the 4 dropout elements 2*pidx .. 2*pidx+3 as multipliers keep/(1-p) or 0 (x * m is the
 // dropout of x, as torch's fused dropout forms it): two hashes, 16 bits per element
 __device__ __forceinline__ f32x4 drop_scale4(const GemmParams& P, uint32_t pidx) {

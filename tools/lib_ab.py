@@ -53,6 +53,8 @@ def main():
         data[name] = (m, n, A, B, sp, ws)
     if os.environ.get("LIB_AB_OP") == "gemm":
         return gemm_mode(libs, g, st)
+    if os.environ.get("LIB_AB_OP") == "attn":
+        return attn_mode(libs, g, st)
     outs = {}
     for i, lib in enumerate(libs):
         for name, (m, n, A, B, sp, ws) in data.items():
@@ -125,6 +127,50 @@ def gemm_mode(libs, g, st):
         for i in range(len(libs)):
             t = sorted(times[(i, name)])[2]
             line += f"  lib{i}: {t * 1e3:8.1f} us {2 * n * k * Mt / t / 1e9:6.0f} TF"
+        print(line, flush=True)
+
+
+def attn_mode(libs, g, st):
+    """LIB_AB_OP=attn: attention forward / backward at cfg 2 (B=64, T=1024, H=12, D=64, dropout 0.1); outputs
+    compared bitwise against the first library."""
+    B, T, H, D = 64, 1024, 12, 64
+    C = H * D
+    qkv = (torch.randn(B * T, 3 * C, device=dev, generator=g) * 0.5).to(torch.bfloat16)
+    dout = (torch.randn(B * T, C, device=dev, generator=g) * 0.1).to(torch.bfloat16)
+    res = []
+    for lib in libs:
+        out = torch.empty(B * T, C, dtype=torch.bfloat16, device=dev)
+        lse = torch.empty(B * H * T, device=dev)
+        delta = torch.empty(B * H * T, device=dev)
+        dqkv = torch.empty(B * T, 3 * C, dtype=torch.bfloat16, device=dev)
+        res.append((out, lse, delta, dqkv))
+    fwd = lambda lib, r: lib.gpt2mi_attn_fwd(qkv.data_ptr(), r[0].data_ptr(), r[1].data_ptr(), B, T, H, D, 0.1,  # noqa
+                                              7, st)
+    bwd = lambda lib, r: lib.gpt2mi_attn_bwd(qkv.data_ptr(), r[0].data_ptr(), dout.data_ptr(), r[1].data_ptr(),  # noqa
+                                              r[2].data_ptr(), r[3].data_ptr(), None, B, T, H, D, 0.1, 7, st)
+    for lib, r in zip(libs, res):
+        assert fwd(lib, r) == 0 and bwd(lib, r) == 0
+    torch.cuda.synchronize()
+    for i in range(1, len(libs)):
+        for k, name in enumerate(("out", "lse", "delta", "dqkv")):
+            if not torch.equal(res[0][k], res[i][k]):
+                print(f"MISMATCH lib{i} {name}")
+    times = {(i, n): [] for i in range(len(libs)) for n in ("fwd", "bwd")}
+    ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+    for _ in range(5):
+        for i, (lib, r) in enumerate(zip(libs, res)):
+            for n, fn in (("fwd", fwd), ("bwd", bwd)):
+                s, e = ev(), ev()
+                s.record()
+                for _r in range(10):
+                    fn(lib, r)
+                e.record()
+                torch.cuda.synchronize()
+                times[(i, n)].append(s.elapsed_time(e) / 10)
+    for n in ("fwd", "bwd"):
+        line = f"attn {n:10s}"
+        for i in range(len(libs)):
+            line += f"  lib{i}: {sorted(times[(i, n)])[2] * 1e3:8.1f} us"
         print(line, flush=True)
 
 
