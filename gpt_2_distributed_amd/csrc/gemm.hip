@@ -211,7 +211,7 @@ int launch(const GemmParams& P, int splits, hipStream_t s) {
 
 // 0 auto (ping-pong 256x256, persistent for short K), 1 force 128x128, 2 force the 2-stage 256x256, 3..5
 // ping-pong with half-tile map 1..3, 6 ping-pong without the persistent schedule, 7 persistent at any K,
-// 8 the ping-pong kernel for the weight gradients too, 9 the ring wgrad kernel
+// 8 = 0 for the weight gradients, 9 the ring wgrad kernel (2 / 9: the weight gradients on gemm256)
 // (A/B experiments, tools/gemm_probe.py, tools/gemm_ab.py)
 static int g_gemm_impl = 0;
 GPT2MI_EXPORT void gpt2mi_set_gemm_impl(int impl) { g_gemm_impl = impl; }
@@ -305,12 +305,17 @@ GPT2MI_EXPORT int gpt2mi_gemm_wgrad(int M, int N, int K, const uint16_t* A, int 
   P.alpha_dev = alpha_dev;
   P.accumulate = accumulate;
   const int ktiles = K / 64;
-  P.k_per_split = ((ktiles + splits - 1) / splits) * 64;
+  // the ping-pong kernel (default; impl 8) walks K-tile pairs: an even tile count per split (the last split's
+  // count is then even too when ktiles is)
+  const bool pp = (g_gemm_impl == 0 || g_gemm_impl == 8) && ktiles % 2 == 0;
+  int tiles_per = (ktiles + splits - 1) / splits;
+  if (pp) tiles_per += tiles_per & 1;
+  P.k_per_split = tiles_per * 64;
   splits = (K + P.k_per_split - 1) / P.k_per_split;
   if (splits == 1) {
     P.C = C;
-    if (g_gemm_impl == 0 || g_gemm_impl >= 3) {
-      const int rc = gpt2mi::gemm_pp_dispatch(2, EPI_F32, P, s, 1, g_gemm_impl == 8 ? 8 : g_gemm_impl >= 3 ? g_gemm_impl - 2 : 0);
+    if (pp) {
+      const int rc = gpt2mi::gemm_pp_dispatch(2, EPI_F32, P, s, 1, g_gemm_impl);
       if (rc >= 0) return rc;
     }
     return gpt2mi::gemm256_dispatch(2, EPI_F32, P, s, 1, g_gemm_impl == 9);
@@ -319,7 +324,7 @@ GPT2MI_EXPORT int gpt2mi_gemm_wgrad(int M, int N, int K, const uint16_t* A, int 
                  "gemm_wgrad: workspace of %zu floats < splits*M*N = %zu", workspace_floats, (size_t)splits * M * N);
   P.C = workspace;
   P.accumulate = 0;
-  int rc = (g_gemm_impl == 0 || g_gemm_impl == 8) ? gpt2mi::gemm_pp_dispatch(2, EPI_SLAB, P, s, splits, g_gemm_impl) : -1;
+  int rc = pp ? gpt2mi::gemm_pp_dispatch(2, EPI_SLAB, P, s, splits, g_gemm_impl) : -1;
   if (rc < 0) rc = gpt2mi::gemm256_dispatch(2, EPI_SLAB, P, s, splits, g_gemm_impl == 9);
   if (rc) return rc;
   return gpt2mi::splitk_reduce(workspace, splits, (size_t)M * N, C, accumulate, s);

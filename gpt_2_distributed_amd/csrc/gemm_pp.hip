@@ -555,11 +555,11 @@ namespace gpt2mi {
 // Returns -1 when this kernel does not apply (the caller falls back).
 int gemm_pp_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t s, int splits, int map) {
   if (P.N % BN != 0 || P.k_per_split % (2 * BK) != 0 || P.K % (2 * BK) != 0) return -1;
-  // wgrad (both operands m-contiguous) runs on the 2-stage gemm256 kernel: this one measured
-  // 698-721 TF vs 765 TF on the lm_head wgrad, 756 vs 852 on qkv (tools/gemm_probe.py, every map)
-  // (map 8: run it anyway, A/B in tools/lib_ab.py)
+  // wgrad (both operands m-contiguous): this kernel since the LDS-DMA went to inline asm (lm_head wgrad 4046 vs
+  // 4485 us on the 2-stage gemm256 kernel, qkv 197 vs 230; before, hipcc's vmcnt(0) drains made it the slower
+  // one, 698-721 vs 765 TF). map 8 = the same (tools/lib_ab.py impl 8)
   if (layout == 2) {
-    if (map != 8) return -1;
+    if (map != 0 && map != 8) return -1;
     return epilogue == EPI_SLAB ? launch<true, true, EPI_SLAB>(P, s, splits)
                                 : epilogue == EPI_F32 ? launch<true, true, EPI_F32>(P, s, 1) : -1;
   }
