@@ -115,8 +115,11 @@ __device__ __forceinline__ f32x4 epilogue_operand(const GemmParams& P, int gm, i
 // Apply the fused epilogue to 4 consecutive outputs C[gm][gn..gn+3]; v = alpha*acc (+bias), opnd =
 // epilogue_operand(gm, gn). TE = element type of the bf16-or-fp32 outputs (C of BF16/GELU/GELU_BWD, aux).
 // Returns the primary output as stored for BF16 / GELU_BWD (for fused column sums), v otherwise.
-template <int EPI, typename TE = bf16>
+// DROPM: -1 tests P.thr per call; 0 / 1 = dropout known off / on (a caller that branches once per tile: the
+// per-row test otherwise splits a pass into exec-masked blocks that cannot interleave).
+template <int EPI, typename TE = bf16, int DROPM = -1>
 __device__ __forceinline__ f32x4 epilogue_apply(const GemmParams& P, int gm, int gn, f32x4 v, f32x4 opnd) {
+  const bool drop = DROPM < 0 ? P.thr != 0u : DROPM == 1;
   const size_t cidx = (size_t)gm * P.ldc + gn;
   // dropout pair index: element gm*N + gn of the logical [M,N] over 2, mod 2^32 (N and gn are multiples of 4
   // in every kernel: N is a multiple of the tile width, host-checked)
@@ -129,14 +132,14 @@ __device__ __forceinline__ f32x4 epilogue_apply(const GemmParams& P, int gm, int
     for (int j = 0; j < 4; ++j) v[j] += opnd[j];
     *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(P.C) + cidx) = v;
   } else if constexpr (EPI == EPI_RESID) {
-    if (P.thr) v *= drop_scale4(P, pidx);
+    if (drop) v *= drop_scale4(P, pidx);
     opnd += v;
     *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(P.C) + cidx) = opnd;
   } else if constexpr (EPI == EPI_GELU) {
     // the forward also emits what the backward needs of this site: dL/du = dL/dh * keep/(1-p) * gelu'(u),
     // so the fc2 dgrad epilogue is one multiply (no dropout hash, no GELU math, no pre-activation)
     f32x4 h, dg, m = {1.f, 1.f, 1.f, 1.f};
-    if (P.thr) m = drop_scale4(P, pidx);
+    if (drop) m = drop_scale4(P, pidx);
     gelu4(v, m, h, dg);
     store4<TE>(reinterpret_cast<TE*>(P.aux) + (size_t)gm * P.ldaux + gn, dg);
     store4<TE>(reinterpret_cast<TE*>(P.C) + cidx, h);

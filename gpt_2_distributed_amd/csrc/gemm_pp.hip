@@ -397,22 +397,19 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
         const int r = it * 8 + wid;
         v[it] = *reinterpret_cast<const f32x4*>(img + r * 256 + 4 * (ch ^ (r & 15)));
       }
+      // every row exists (M % 256 == 0, host-checked) and dropout is decided once per pass: straight-line rows
+      auto rows = [&](auto drop_c) {
 #pragma unroll
-      for (int it = 0; it < 8; ++it) {
-        const int gm = m0 + q * 64 + it * 8 + wid;
-        if (gm < P.M) {
+        for (int it = 0; it < 8; ++it) {
+          const int gm = m0 + q * 64 + it * 8 + wid;
           f32x4 w = v[it];
 #pragma unroll
           for (int e = 0; e < 4; ++e) w[e] += bias[e];
-          const f32x4 o = epilogue_apply<EPI>(P, gm, gn, w, kOpnd ? opnd[it] : f32x4{0.f, 0.f, 0.f, 0.f});
-          if constexpr (kCsum) {
-            if (csum_on) {
-#pragma unroll
-              for (int e = 0; e < 4; ++e) csum[e] += o[e];
-            }
-          }
+          epilogue_apply<EPI, bf16, decltype(drop_c)::value>(P, gm, gn, w, kOpnd ? opnd[it] : f32x4{0.f, 0.f, 0.f, 0.f});
         }
-      }
+      };
+      if (P.thr) rows(std::integral_constant<int, 1>{});
+      else rows(std::integral_constant<int, 0>{});
     }
   } else {
 #pragma unroll
@@ -447,7 +444,10 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
       const int r = it * 8 + wid;
       return m0 + (AIL ? ((r >> 6) << 7) + mi * 64 + (r & 63) : mi * 128 + r);
     };
-    auto finish = [&](int it, f32x4 v) {
+    // VC: the per-tile switch known at compile time in the full-tile path — dropout for RESID / GELU, the fused
+    // column sums for BF16 / GELU_BWD (-1: tested per row)
+    auto finish = [&](int it, f32x4 v, auto vc) {
+      constexpr int VC = decltype(vc)::value;
       const int gm = row_of(it);
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] += bias[e];
@@ -455,9 +455,10 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
         float* slab = reinterpret_cast<float*>(P.C) + (size_t)split * P.M * P.ldc;
         *reinterpret_cast<f32x4*>(slab + (size_t)gm * P.ldc + gn) = v;
       } else {
-        const f32x4 o = epilogue_apply<EPI>(P, gm, gn, v, kOpnd ? opnd[it] : f32x4{0.f, 0.f, 0.f, 0.f});
+        constexpr int DROPM = (EPI == EPI_RESID || EPI == EPI_GELU) ? VC : -1;
+        const f32x4 o = epilogue_apply<EPI, bf16, DROPM>(P, gm, gn, v, kOpnd ? opnd[it] : f32x4{0.f, 0.f, 0.f, 0.f});
         if constexpr (kCsum) {
-          if (csum_on) {
+          if (VC < 0 ? csum_on : VC == 1) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) csum[e] += o[e];
           }
@@ -471,13 +472,18 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
         const int r = it * 8 + wid;
         v[it] = *reinterpret_cast<const f32x4*>(img + r * 256 + 4 * (ch ^ (r & 15)));
       }
+      auto rows = [&](auto vc) {
 #pragma unroll
-      for (int it = 0; it < 16; ++it) finish(it, v[it]);
+        for (int it = 0; it < 16; ++it) finish(it, v[it], vc);
+      };
+      const bool on = (EPI == EPI_RESID || EPI == EPI_GELU) ? P.thr != 0u : csum_on;
+      if (on) rows(std::integral_constant<int, 1>{});
+      else rows(std::integral_constant<int, 0>{});
     } else {
       for (int it = 0; it < 16; ++it) {
         const int r = it * 8 + wid;
         const f32x4 v = *reinterpret_cast<const f32x4*>(img + r * 256 + 4 * (ch ^ (r & 15)));
-        if (row_of(it) < P.M) finish(it, v);
+        if (row_of(it) < P.M) finish(it, v, std::integral_constant<int, -1>{});
       }
     }
   }

@@ -96,24 +96,34 @@ def main():
 def gemm_mode(libs, g, st):
     """LIB_AB_OP=gemm: forward / dgrad layouts (gpt2mi_gemm, BF16 epilogue) on the lm_head and K=768 shapes."""
     Mt, C, Vp = 65536, 768, 50432
-    # name: (layout, N, K)
-    shapes = {"lm_head fwd": (0, Vp, C), "lm_head dgrad": (1, C, Vp), "qkv fwd": (0, 3 * C, C), "fc1 dgrad": (1, C, 4 * C)}
+    # name: (layout, N, K, epilogue); the fused-epilogue shapes run as in the step (bias, p = 0.1)
+    shapes = {"lm_head fwd": (0, Vp, C, K.EPI_BF16), "lm_head dgrad": (1, C, Vp, K.EPI_BF16),
+              "qkv fwd": (0, 3 * C, C, K.EPI_BF16), "fc1 dgrad": (1, C, 4 * C, K.EPI_BF16),
+              "fc1 gelu": (0, 4 * C, C, K.EPI_GELU), "fc2dg gelubwd": (0, 4 * C, C, K.EPI_GELU_BWD),
+              "proj resid": (0, C, C, K.EPI_RESID), "fc2 resid": (0, C, 4 * C, K.EPI_RESID)}
+    if os.environ.get("GEMM_AB_SHAPES"):
+        shapes = {k: v for k, v in shapes.items() if any(t in k for t in os.environ["GEMM_AB_SHAPES"].split(","))}
     data = {}
-    for name, (lay, n, k) in shapes.items():
+    for name, (lay, n, k, epi) in shapes.items():
         A = (torch.randn(Mt, k, device=dev, generator=g) * 0.1).to(torch.bfloat16)
         B = (torch.randn(n, k, device=dev, generator=g) if lay == 0 else
              torch.randn(k, n, device=dev, generator=g)).to(torch.bfloat16)
-        out = torch.empty(Mt, n, dtype=torch.bfloat16, device=dev)
-        data[name] = (lay, n, k, A, B, out)
+        out = torch.empty(Mt, n, dtype=torch.float32 if epi == K.EPI_RESID else torch.bfloat16, device=dev)
+        bias = torch.randn(n, device=dev, generator=g) if epi != K.EPI_BF16 else None
+        resid = torch.randn(Mt, n, device=dev, generator=g) if epi == K.EPI_RESID else None
+        aux = torch.randn(Mt, n, device=dev, generator=g).to(torch.bfloat16) if epi in (K.EPI_GELU, K.EPI_GELU_BWD) else None
+        data[name] = (lay, n, k, A, B, out, epi, bias, resid, aux)
     times = {(i, n): [] for i in range(len(libs)) for n in shapes}
     ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+    ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
     for _ in range(5):
-        for name, (lay, n, k, A, B, out) in data.items():
+        for name, (lay, n, k, A, B, out, epi, bias, resid, aux) in data.items():
             ldb = k if lay == 0 else n
+            pd = 0.1 if epi in (K.EPI_GELU, K.EPI_RESID) else 0.0
             for i, lib in enumerate(libs):
-                fn = lambda: lib.gpt2mi_gemm(lay, 0, Mt, n, k, A.data_ptr(), k, B.data_ptr(), ldb,  # noqa: E731
-                                             out.data_ptr(), n, None, None, None, 0, 1.0, None, 0, 1, 0.0, 0,
-                                             None, st)
+                fn = lambda: lib.gpt2mi_gemm(lay, epi, Mt, n, k, A.data_ptr(), k, B.data_ptr(), ldb,  # noqa: E731
+                                             out.data_ptr(), n, ptr(bias), ptr(resid), ptr(aux), n if aux is not None else 0,
+                                             1.0, None, 0, 1, pd, 5, None, st)
                 assert fn() == 0
                 s, e = ev(), ev()
                 s.record()
@@ -123,7 +133,7 @@ def gemm_mode(libs, g, st):
                 torch.cuda.synchronize()
                 times[(i, name)].append(s.elapsed_time(e) / 5)
     for name, (lay, n, k, *_r) in data.items():
-        line = f"{name:14s}"
+        line = f"{name:15s}"
         for i in range(len(libs)):
             t = sorted(times[(i, name)])[2]
             line += f"  lib{i}: {t * 1e3:8.1f} us {2 * n * k * Mt / t / 1e9:6.0f} TF"
