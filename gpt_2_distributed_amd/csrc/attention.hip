@@ -271,12 +271,12 @@ __global__ __launch_bounds__(kThreads, DROP ? 4 : 3) void attn_fwd_kernel(const 
       if constexpr (DROP) {  // dropout on P (not on the normaliser; the 1/(1-p) goes into the final scale): one
                   // hash per (q, q^16) pair of a key
         const uint32_t s32 = seed32(seed);
-        const uint32_t pbase = ((uint32_t)bh * T + q_lo + (lane & 15)) * (uint32_t)T + k_lo + 4 * g;
+        const uint32_t pre = drop_pre(s32, ((uint32_t)bh * T + q_lo + (lane & 15)) * (uint32_t)T + k_lo + 4 * g);
 #pragma unroll
         for (int fi = 0; fi < 4; ++fi)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const uint32_t hh = drop_hash(s32, pbase + 16 * fi + r);
+            const uint32_t hh = drop_fin(pre + (uint32_t)(16 * fi + r) * kDropC1);
             if (!drop_keep16(hh, 0, thr)) s[0][fi][r] = 0.f;
             if (!drop_keep16(hh, 1, thr)) s[1][fi][r] = 0.f;
           }
@@ -401,17 +401,15 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const bf16* __
       // dS^T = P^T o (dP'^T - delta): dropped entries get dP = 0 (same (q, q^16)-pair hash as the forward)
       auto elementwise = [&](auto diag_c) {
         constexpr bool DIAG = decltype(diag_c)::value;
-        uint32_t pbase = 0, s32 = 0;
-        if constexpr (DROP) {
-          s32 = seed32(seed);
-          pbase = ((uint32_t)bh * T + q_lo + (lane & 15)) * (uint32_t)T + k_lo + 4 * g;
-        }
+        uint32_t pre = 0;
+        if constexpr (DROP)
+          pre = drop_pre(seed32(seed), ((uint32_t)bh * T + q_lo + (lane & 15)) * (uint32_t)T + k_lo + 4 * g);
 #pragma unroll
         for (int fi = 0; fi < 4; ++fi)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             uint32_t hh = 0;
-            if constexpr (DROP) hh = drop_hash(s32, pbase + 16 * fi + r);
+            if constexpr (DROP) hh = drop_fin(pre + (uint32_t)(16 * fi + r) * kDropC1);
 #pragma unroll
             for (int qg = 0; qg < 2; ++qg) {
               float p = __builtin_amdgcn_exp2f(fmaf(s[qg][fi][r], sl2, -lse2[qg]));
@@ -532,7 +530,7 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dkdv_kernel(const bf16* 
     const int q0 = i * BQT;
     if (wave_valid && q0 + BQT - 1 >= k_lo) {  // wave-uniform: a query of the tile sees a key of the wave
       const bool diag = q0 < k_lo + 31;
-      const uint32_t s32 = seed32(seed);
+      const uint32_t pre_t = DROP ? drop_pre(seed32(seed), ((uint32_t)bh * T + q0 + 4 * g) * (uint32_t)T + k_lo + (lane & 15)) : 0u;
       // Two 32-query halves per 64-query tile; each half is exactly one MFMA k-step of the dV/dK
       // products, so only half of S / dP is live at a time (register pressure -> occupancy).
 #pragma unroll
@@ -569,7 +567,8 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dkdv_kernel(const bf16* 
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               uint32_t hh = 0;  // queries q and q^16 (fl = 0, 1) share one dropout hash
-              if constexpr (DROP) hh = drop_hash(s32, ((uint32_t)bh * T + q0 + 32 * hq + 4 * g + r) * (uint32_t)T + key);
+              // counter (bh*T + q0 + 4g + 32hq + r) * T + key: a lane base plus (32hq + r) * T + 16kg (uniform)
+              if constexpr (DROP) hh = drop_fin(pre_t + ((uint32_t)(32 * hq + r) * (uint32_t)T + 16u * kg) * kDropC1);
 #pragma unroll
               for (int fl = 0; fl < 2; ++fl) {
                 float p = __builtin_amdgcn_exp2f(fmaf(s[kg][fl][r], sl2, -l4[fl][r]));

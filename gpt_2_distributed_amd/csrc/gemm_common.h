@@ -35,7 +35,8 @@ struct GemmParams {
 // dropout of x, as torch's fused dropout forms it): two hashes, 16 bits per element
 __device__ __forceinline__ f32x4 drop_scale4(const GemmParams& P, uint32_t pidx) {
   const uint32_t s = seed32(P.seed);
-  const uint32_t h0 = drop_hash(s, pidx), h1 = drop_hash(s, pidx + 1u);
+  const uint32_t pre = drop_pre(s, pidx);
+  const uint32_t h0 = drop_fin(pre), h1 = drop_fin(pre + kDropC1);
   const float k = P.inv_keep;
   return f32x4{drop_keep16(h0, 0, P.thr) ? k : 0.f, drop_keep16(h0, 1, P.thr) ? k : 0.f,
                drop_keep16(h1, 0, P.thr) ? k : 0.f, drop_keep16(h1, 1, P.thr) ? k : 0.f};

@@ -35,8 +35,8 @@ def threshold(p: float) -> int:
 
 
 def drop_hash(s32: np.uint32, x: np.ndarray) -> np.ndarray:
-    """Two multiply-xorshift rounds over uint32 (csrc/common.h drop_hash)."""
-    h = (x.astype(np.uint64) ^ np.uint64(s32)) * np.uint64(0x9E3779B1) & M32
+    """Two multiply-xorshift rounds over uint32 (csrc/common.h drop_hash; first round (x + s32) * C1)."""
+    h = ((x.astype(np.uint64) + np.uint64(s32)) & M32) * np.uint64(0x9E3779B1) & M32
     h ^= h >> np.uint64(16)
     h = h * np.uint64(0x85EBCA6B) & M32
     h ^= h >> np.uint64(13)

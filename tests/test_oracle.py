@@ -110,7 +110,7 @@ def test_dropout_restatement():
     from oracle import dropout_ref as D
 
     def h_py(s, x):
-        h = ((x ^ s) * 0x9E3779B1) & 0xFFFFFFFF
+        h = (((x + s) & 0xFFFFFFFF) * 0x9E3779B1) & 0xFFFFFFFF
         h ^= h >> 16
         h = (h * 0x85EBCA6B) & 0xFFFFFFFF
         return h ^ (h >> 13)
@@ -121,6 +121,14 @@ def test_dropout_restatement():
     xs = np.array([0, 1, 2, 12345, 2**31 + 7, 2**32 - 1], dtype=np.uint64)
     assert [int(v) for v in D.drop_hash(D.seed32(seed), xs)] == [h_py(s32, int(x)) for x in xs]
     assert D.threshold(0.1) == 6554 and D.threshold(0.0) == 0
+    # no correlation between the decisions of neighbouring counters along the strides the kernels walk
+    # (adjacent keys, the next query row at T = 1024, the next 32-query half, the paired query q ^ 16)
+    x = np.arange(1 << 20, dtype=np.uint64) * np.uint64(3) + np.uint64(977)
+    keep = lambda idx, half: D._keep(D.drop_hash(np.uint32(s32), idx), np.full(idx.shape, half), 6554)  # noqa
+    base = keep(x, 0).astype(np.float64)
+    for stride, half in ((1, 0), (1024, 0), (32 * 1024, 0), (0, 1)):
+        other = keep(x + np.uint64(stride), half).astype(np.float64)
+        assert abs(float(np.corrcoef(base, other)[0, 1])) < 0.01, (stride, half)
     m = D.site_scale(seed, 256, 768, 0.1)
     assert abs(float((m == 0).float().mean()) - 0.1) < 0.005
     assert torch.allclose(m[m > 0], torch.tensor(1 / 0.9))

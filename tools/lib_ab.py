@@ -145,6 +145,7 @@ def attn_mode(libs, g, st):
     compared bitwise against the first library."""
     B, T, H, D = 64, 1024, 12, 64
     C = H * D
+    pd = float(os.environ.get("LIB_AB_PDROP", "0.1"))
     qkv = (torch.randn(B * T, 3 * C, device=dev, generator=g) * 0.5).to(torch.bfloat16)
     dout = (torch.randn(B * T, C, device=dev, generator=g) * 0.1).to(torch.bfloat16)
     res = []
@@ -154,10 +155,10 @@ def attn_mode(libs, g, st):
         delta = torch.empty(B * H * T, device=dev)
         dqkv = torch.empty(B * T, 3 * C, dtype=torch.bfloat16, device=dev)
         res.append((out, lse, delta, dqkv))
-    fwd = lambda lib, r: lib.gpt2mi_attn_fwd(qkv.data_ptr(), r[0].data_ptr(), r[1].data_ptr(), B, T, H, D, 0.1,  # noqa
+    fwd = lambda lib, r: lib.gpt2mi_attn_fwd(qkv.data_ptr(), r[0].data_ptr(), r[1].data_ptr(), B, T, H, D, pd,  # noqa
                                               7, st)
     bwd = lambda lib, r: lib.gpt2mi_attn_bwd(qkv.data_ptr(), r[0].data_ptr(), dout.data_ptr(), r[1].data_ptr(),  # noqa
-                                              r[2].data_ptr(), r[3].data_ptr(), None, B, T, H, D, 0.1, 7, st)
+                                              r[2].data_ptr(), r[3].data_ptr(), None, B, T, H, D, pd, 7, st)
     for lib, r in zip(libs, res):
         assert fwd(lib, r) == 0 and bwd(lib, r) == 0
     torch.cuda.synchronize()
