@@ -101,8 +101,10 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 // does not look inside asm: s_nop 4 covers the M0-write -> LDS-DMA (1) and VALU-SGPR-write -> VMEM-read (5) wait
 // states of the SGPR operands (descriptor, soffset, M0).
 typedef __attribute__((address_space(3))) void lds_void;
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {  // generic pointer into LDS -> LDS byte address
-  return (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const lds_void*)p);
+// generic pointer into LDS -> LDS byte address: the shared aperture is 4 GiB aligned, so the low 32 bits of a
+// flat LDS address are the LDS offset (a plain truncation; the address-space cast would add a null check per DMA)
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)p);
 }
 __device__ __forceinline__ void lds_dma16(const void* gptr, const void* lds_dst) {
   const uint32_t m0 = lds_addr(lds_dst);

@@ -154,6 +154,9 @@ __device__ __forceinline__ void mfma_quadrant(f32x4 (&acc)[4][2], const Frags& f
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.b[NI][kk][j], f.a[kk][i], acc[i][j], 0, 0, 0);
 }
 
+// s_waitcnt vmcnt takes 0..63: a count past that waits for a few more of the oldest operations (safe)
+constexpr int vm_cap(int n) { return n > 63 ? 63 : n; }
+
 // end of a phase's memory segment: retire the half-tile the next phase reads, then the ping-pong
 // MFMA segment between two barriers
 #define PP_SYNC_MFMA(ACC, NI, VM)                          \
@@ -167,6 +170,21 @@ __device__ __forceinline__ void mfma_quadrant(f32x4 (&acc)[4][2], const Frags& f
   __builtin_amdgcn_s_setprio(0);                           \
   __builtin_amdgcn_sched_barrier(0);                       \
   __builtin_amdgcn_s_barrier();                            \
+  __builtin_amdgcn_sched_barrier(0);
+
+// the same with the wait chosen at run time: vmcnt(VM + kStores) when FIRST (persistent K-tile 0), else vmcnt(VM)
+#define PP_SYNC_MFMA_F(ACC, NI, VM, FIRST)                                             \
+  if (FIRST) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(vm_cap((VM) + kStores)) : "memory"); \
+  else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM) : "memory");                       \
+  __builtin_amdgcn_sched_barrier(0);                                                  \
+  __builtin_amdgcn_s_barrier();                                                       \
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                  \
+  __builtin_amdgcn_sched_barrier(0);                                                  \
+  __builtin_amdgcn_s_setprio(1);                                                      \
+  mfma_quadrant<NI>(ACC, fr);                                                         \
+  __builtin_amdgcn_s_setprio(0);                                                      \
+  __builtin_amdgcn_sched_barrier(0);                                                  \
+  __builtin_amdgcn_s_barrier();                                                       \
   __builtin_amdgcn_sched_barrier(0);
 
 // workgroup barrier that orders LDS only (the epilogue's global stores stay in flight)
@@ -231,6 +249,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   const int kbeg = split * P.k_per_split;
   const int nk = (min(P.K, kbeg + P.k_per_split) - kbeg) / BK;  // even (host-checked)
 
+  // PERSIST: vector-memory stores each wave issues in an epilogue (one per output row and output array)
+  constexpr int kStores = EPI == EPI_GELU ? 64 : 32;
+  bool after_epi = false;  // the current tile follows an epilogue (wave-uniform)
   f32x4 acc[2][2][4][2];
   auto zero_acc = [&]() {
 #pragma unroll
@@ -291,9 +312,18 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   // (LAST) the DMAs for tiles >= nk are not issued, and each wait retires what the next phase reads
   // from the real DMAs still outstanding (vmcnt 8,8,6,4 | 2,0,0,0 instead of 8 everywhere): no re-load
   // traffic, and nothing left in flight for the epilogue to wait for.
+  //
+  // FIRST (persistent schedule, K-tile 0 of a tile after an epilogue): the waits of phases 1-2 retire half-tiles
+  // issued BEFORE the previous tile's epilogue stores. vmcnt counts loads, stores and LDS-DMA together in issue
+  // order and waits for all but the N youngest, so those waits count the epilogue's kStores stores among the
+  // younger operations instead of draining them: the stores get two more phases to complete in the background.
   auto ktile = [&](int t, auto s_c, auto last_c) {
     constexpr int S = decltype(s_c)::value;
     constexpr bool LAST = decltype(last_c)::value;
+    // PERSIST, K-tile 0 (t == 0, S == 0) of a tile that follows an epilogue: phases 1-2 wait with the epilogue's
+    // stores counted as younger (a wave-uniform branch around the wait alone; nk >= 4 host-checked, so K-tile 0
+    // is never in the LAST pair)
+    const bool first = PERSIST && S == 0 && !LAST && t == 0 && after_epi;
     constexpr bool next_dma = !LAST || S == 0;  // tile tt + 1 exists
     constexpr bool next2_dma = !LAST;           // tile tt + 2 exists
     char* cur = S ? buf1 : buf0;
@@ -303,11 +333,11 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
     read_a<A_T>(fr, cur + SA0, wr, lane);
     read_b<B_T, 0>(fr, cur + SB0, wc, lane);
     if constexpr (next_dma) dma_b(tt + 1, 1, nxt);
-    PP_SYNC_MFMA(acc[0][0], 0, (!LAST || S == 0) ? 8 : 2)
+    PP_SYNC_MFMA_F(acc[0][0], 0, (!LAST || S == 0) ? 8 : 2, first)
     // phase 2: quadrant (0,1)
     read_b<B_T, 1>(fr, cur + SB1, wc, lane);
     if constexpr (next_dma) dma_a(tt + 1, 1, nxt);
-    PP_SYNC_MFMA(acc[0][1], 1, (!LAST || S == 0) ? 8 : 0)
+    PP_SYNC_MFMA_F(acc[0][1], 1, (!LAST || S == 0) ? 8 : 0, first)
     // phase 3: quadrant (1,1)
     read_a<A_T>(fr, cur + SA1, wr, lane);
     if constexpr (next2_dma) dma_a(tt + 2, 0, cur);
@@ -318,12 +348,14 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   };
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
+  using F = std::false_type;
+  using Tr = std::true_type;
   for (int t = 0; t < nk - 2; t += 2) {
-    ktile(t, I0{}, std::false_type{});
-    ktile(t, I1{}, std::false_type{});
+    ktile(t, I0{}, F{});
+    ktile(t, I1{}, F{});
   }
-  ktile(nk - 2, I0{}, std::true_type{});
-  ktile(nk - 2, I1{}, std::true_type{});
+  ktile(nk - 2, I0{}, Tr{});
+  ktile(nk - 2, I1{}, Tr{});
   if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the groups (same barrier count)
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
@@ -515,10 +547,13 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
     zero_acc();
     dma_a(1, 0, buf1);
     dma_b(1, 0, buf1);
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    // K-tile 0's A_0 / B_0 landed; its B_1 / A_1, the epilogue's kStores stores and K-tile 1's A_0 / B_0 are the
+    // younger operations that may stay in flight (see FIRST above)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(vm_cap(8 + kStores)) : "memory");
     __builtin_amdgcn_s_barrier();
     if (wr == 1) __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
+    after_epi = true;
   }
   }  // tile loop
 }
@@ -583,7 +618,7 @@ int gemm_pp_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t 
   // short-K forward-layout shapes with no epilogue operand loads: the persistent schedule (map < 0 forces
   // the one-tile-per-block kernel, map 7 the persistent one at any K: tools/gemm_ab.py)
   const int ntiles = ((P.M + BM - 1) / BM) * (P.N / BN);
-  if (layout == 0 && (map == 0 || map == 7) && (P.K <= 1024 || map == 7) && ntiles >= 2 * num_cus() &&
+  if (layout == 0 && (map == 0 || map == 7) && (P.K <= 1024 || map == 7) && P.K >= 4 * BK && ntiles >= 2 * num_cus() &&
       P.dbias == nullptr &&
       (epilogue == EPI_BF16 || epilogue == EPI_GELU) && P.M % BM == 0 && (size_t)P.M * P.lda * 2 < (1ull << 31) &&
       (size_t)P.N * P.ldb * 2 < (1ull << 31)) {
