@@ -46,6 +46,7 @@ _SIGS = {
     "gpt2mi_scale_mul": [_p, _p, _p, _p],
     "gpt2mi_memset_zero": [_p, _c_size, _p],
     "gpt2mi_set_gemm_impl": [_c_int],
+    "gpt2mi_set_gemm_persistent": [_c_int],
     "gpt2mi_gemm_f32": [_c_int, _c_int, _c_int, _c_int, _c_int, _p, _c_int, _p, _c_int, _p, _c_int, _p, _p, _p,
                         _c_int, _c_float, _p, _c_int, _c_int, _c_float, _c_u64, _p, _p],
     "gpt2mi_attn_fwd_f32": [_p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_float, _c_u64, _p],
@@ -66,7 +67,7 @@ _SIGS = {
     "gpt2mi_gemm_wgrad": [_c_int, _c_int, _c_int, _p, _c_int, _p, _c_int, _p, _c_int, _c_int, _c_float, _p, _p,
                           _c_size, _c_int, _p],
 }
-_RESTYPES = {"gpt2mi_last_error": ctypes.c_char_p, "gpt2mi_set_gemm_impl": None}
+_RESTYPES = {"gpt2mi_last_error": ctypes.c_char_p, "gpt2mi_set_gemm_impl": None, "gpt2mi_set_gemm_persistent": None}
 
 EXPORTED = tuple(_SIGS)
 
@@ -282,3 +283,8 @@ def zero_(t: torch.Tensor):
 def set_gemm_impl(impl: int):
     """0 = auto (256x256 kernel where it applies), 1 = force the 128x128 kernel (A/B benchmarking)."""
     load().gpt2mi_set_gemm_impl(impl)
+
+
+def set_gemm_persistent(on: bool):
+    """Allow (default) or forbid the persistent GEMM schedule in the auto selection (gpt2mi.h)."""
+    load().gpt2mi_set_gemm_persistent(int(bool(on)))

@@ -215,6 +215,10 @@ int launch(const GemmParams& P, int splits, hipStream_t s) {
 // (A/B experiments, tools/gemm_probe.py, tools/gemm_ab.py)
 static int g_gemm_impl = 0;
 GPT2MI_EXPORT void gpt2mi_set_gemm_impl(int impl) { g_gemm_impl = impl; }
+namespace gpt2mi {
+bool g_gemm_persistent = true;
+}
+GPT2MI_EXPORT void gpt2mi_set_gemm_persistent(int on) { gpt2mi::g_gemm_persistent = on != 0; }
 
 // layout: 0 = forward (A[M][K], B[N][K]); 1 = dgrad (A[M][K], B[K][N]); 2 = wgrad (A[K][M], B[K][N]).
 GPT2MI_EXPORT int gpt2mi_gemm(int layout, int epilogue, int M, int N, int K, const uint16_t* A, int lda,

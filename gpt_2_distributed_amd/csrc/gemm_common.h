@@ -164,6 +164,7 @@ __device__ __forceinline__ void epilogue_store(const GemmParams& P, int gm, int 
 }
 
 namespace gpt2mi {
+extern bool g_gemm_persistent;  // gpt2mi_set_gemm_persistent
 // ring: the weight-gradient GEMMs (layout 2) on the 5-slot half-K-tile ring kernel
 int gemm256_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t s, int splits, bool ring = false);
 int gemm_pp_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t s, int splits, int map = 0);

@@ -618,7 +618,8 @@ int gemm_pp_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t 
   // short-K forward-layout shapes with no epilogue operand loads: the persistent schedule (map < 0 forces
   // the one-tile-per-block kernel, map 7 the persistent one at any K: tools/gemm_ab.py)
   const int ntiles = ((P.M + BM - 1) / BM) * (P.N / BN);
-  if (layout == 0 && (map == 0 || map == 7) && (P.K <= 1024 || map == 7) && P.K >= 4 * BK && ntiles >= 2 * num_cus() &&
+  if (layout == 0 && (map == 7 || (map == 0 && g_gemm_persistent && P.K <= 1024)) && P.K >= 4 * BK &&
+      ntiles >= 2 * num_cus() &&
       P.dbias == nullptr &&
       (epilogue == EPI_BF16 || epilogue == EPI_GELU) && P.M % BM == 0 && (size_t)P.M * P.lda * 2 < (1ull << 31) &&
       (size_t)P.N * P.ldb * 2 < (1ull << 31)) {

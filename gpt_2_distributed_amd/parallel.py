@@ -185,6 +185,14 @@ class _DDPHooks(_DPHooks):
         super().__init__(engine, world)
         self.reducer = reducer
 
+    def begin_backward(self) -> float:
+        if self.sync and self.coll:
+            # the buckets' RCCL kernels run under the rest of the backward: no persistent GEMM grid there
+            # (a block waiting for a CU held by a collective would hold the whole grid back; gpt2mi.h)
+            from . import _lib as K
+            K.set_gemm_persistent(False)
+        return super().begin_backward()
+
     def ready(self, name):
         if self.sync and self.coll:
             self.reducer.mark_ready(name)
@@ -192,6 +200,8 @@ class _DDPHooks(_DPHooks):
     def end_backward(self):
         if self.sync and self.coll:
             self.reducer.finish()
+            from . import _lib as K
+            K.set_gemm_persistent(True)
 
 
 class DistributedDataParallel(nn.Module):
@@ -293,6 +303,10 @@ class FullyShardedDataParallel(nn.Module):
         self.coll = use_collectives(W)
         if self.coll:
             dist.broadcast(module.arena, src=0)
+            # prefetched all-gathers and reduce-scatters overlap the forward and the backward: no persistent
+            # GEMM grids in this process (see _DDPHooks.begin_backward)
+            from . import _lib as K
+            K.set_gemm_persistent(False)
         self.units = unit_ranges(module.layout, module.config.n_layer)
         self.plans, self.shard_total = plan_shards(self.units, W)
         self.plan = {p.name: p for p in self.plans}

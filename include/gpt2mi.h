@@ -136,6 +136,10 @@ int gpt2mi_xent_fwd_f32(const float* logits, int ld, const int64_t* labels, floa
 /* GEMM kernel selection for A/B benchmarking: 0 = auto (256x256 tiles for layouts 0/1 when N % 256 == 0),
  * 1 = always the 128x128 kernel. */
 void gpt2mi_set_gemm_impl(int impl);
+/* 1 (default) lets the auto selection use the persistent GEMM schedule (one block per CU walking the tiles); 0 turns
+ * it off. The data-parallel wrappers turn it off while their RCCL kernels may run concurrently: a block that lands
+ * on a CU held by a collective would wait for it, and a persistent grid ends on its latest block. */
+void gpt2mi_set_gemm_persistent(int on);
 
 /* dst[c][r] = src[r][c] for a bf16 [R][C] matrix (R, C multiples of 64): the transposed weight shadow
  * the backward dgrad GEMMs read in the forward (k-contiguous) layout. */
