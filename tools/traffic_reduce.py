@@ -21,7 +21,7 @@ ALGO = {  # algorithmic bytes per launch (operands read once, outputs written on
     "attn_fwd": 2 * (65536 * 2304 + 65536 * 768) + 4 * 768 * 1024,
 }
 # kernels whose counters make up one probed launch (the wgrad probe = split-K GEMM + slab reduction)
-KERNEL_KEY = {"attn_fwd": ("attn_fwd",), "lm_head_wgrad": ("gemm256", "splitk_reduce")}
+KERNEL_KEY = {"attn_fwd": ("attn_fwd",), "lm_head_wgrad": ("gemm_pp", "splitk_reduce")}
 
 
 def short(name):
