@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GPT2MI_ABI_VERSION 5
+#define GPT2MI_ABI_VERSION 6
 
 const char* gpt2mi_last_error(void);
 int gpt2mi_abi_version(void); /* returns GPT2MI_ABI_VERSION of the built library */

@@ -519,8 +519,9 @@ def test_gemm_persistent_schedule_bitwise(epi, M, N):
     W = bf(torch.randn(N, K, generator=g) * 0.05).to(dev)
     bias = torch.randn(N, generator=g).to(dev) if epi != "plain" else None
     outs = []
-    for impl in (0, 6):
+    for impl, persistent in ((0, True), (6, True), (0, False)):  # (0, False): the wrappers' no-persistent switch
         L().set_gemm_impl(impl)
+        L().set_gemm_persistent(persistent)
         try:
             C = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
             if epi == "gelu_drop":
@@ -533,10 +534,39 @@ def test_gemm_persistent_schedule_bitwise(epi, M, N):
                 outs.append((C,))
         finally:
             L().set_gemm_impl(0)
+            L().set_gemm_persistent(True)
     torch.cuda.synchronize()
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)
+    for other in outs[1:]:
+        for a, b in zip(outs[0], other):
+            assert torch.equal(a, b)
     rows = torch.arange(0, M, M // 64, device=dev)
     ref = A[rows].float() @ W.float().t() + (bias if bias is not None else 0.0)
     if epi != "gelu_drop":
         assert rel_err(outs[0][0][rows].float().cpu(), ref.cpu()) < 4e-3
+
+
+@pytest.mark.parametrize("m,n,tokens,splits", [(2304, 768, 8192, 4), (768, 3072, 8192, 8), (50432, 768, 4096, 3)])
+def test_wgrad_kernels_bitwise(m, n, tokens, splits):
+    """The weight gradient on the ping-pong kernel (default), the 2-stage 256x256 kernel (impl 2) and the 5-slot
+    ring kernel (impl 9): the same K order per output element (split counts chosen so every kernel cuts K at the
+    same K-tiles), so bitwise equal; and within fp32 rounding of a float64 reference on sampled rows."""
+    g = torch.Generator().manual_seed(m + n + splits)
+    A = bf(torch.randn(tokens, m, generator=g) * 0.1).to(dev)
+    B = bf(torch.randn(tokens, n, generator=g)).to(dev)
+    ws = torch.empty(splits * m * n, device=dev)
+    outs = []
+    for impl in (0, 2, 9):
+        L().set_gemm_impl(impl)
+        try:
+            C = torch.zeros(m, n, device=dev)
+            L().gemm_wgrad(m, n, tokens, A, m, B, n, C, n, accumulate=True, workspace=ws, splits=splits)
+            outs.append(C)
+        finally:
+            L().set_gemm_impl(0)
+    torch.cuda.synchronize()
+    for o in outs[1:]:
+        assert torch.equal(outs[0], o)
+    rows = torch.arange(0, m, max(1, m // 32), device=dev)
+    ref = A[:, rows].double().t() @ B.double()
+    err = (outs[0][rows].double() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 1e-5, err
