@@ -55,17 +55,18 @@ __device__ __forceinline__ float wave_max(float v) {
 // which sit in the same lane in every attention kernel). keep = uniform16 >= round(p * 2^16).
 // All element / pair indices fit in 32 bits for every BASELINE config (attention B*H*T*T < 2^32).
 __device__ __forceinline__ uint32_t seed32(uint64_t seed) { return (uint32_t)seed ^ (uint32_t)(seed >> 32); }
-// Two rounds of multiply-xorshift (murmur3 fmix32 without its last multiply). The first round is linear in the
+// Two rounds of multiply-xorshift (murmur3 fmix32 without its closing rounds). The first round is linear in the
 // counter, (x + s32) * C1, so a kernel walking counters x + c (c a per-element constant) forms it as
 // drop_pre(s32, x) + c * C1: one v_add instead of an add, xor and v_mul_lo_u32 (half the VALU rate, measured by
 // tools/valu_probe.hip) per hash.
 constexpr uint32_t kDropC1 = 0x9E3779B1u, kDropC2 = 0x85EBCA6Bu;
 __device__ __forceinline__ uint32_t drop_pre(uint32_t s32, uint32_t x) { return (x + s32) * kDropC1; }
+// The second round ends at the multiply: a closing xorshift (murmur3's h ^= h >> 13) leaves the 16-bit decisions
+// statistically unchanged (tests/test_oracle.py: decision correlations over the kernels' counter strides) and
+// costs three instructions per hash in the attention kernels.
 __device__ __forceinline__ uint32_t drop_fin(uint32_t h) {
   h ^= h >> 16;
-  h *= kDropC2;
-  h ^= h >> 13;
-  return h;
+  return h * kDropC2;
 }
 __device__ __forceinline__ uint32_t drop_hash(uint32_t s32, uint32_t x) { return drop_fin(drop_pre(s32, x)); }
 __device__ __forceinline__ bool drop_keep16(uint32_t h, int half, uint32_t thr) {

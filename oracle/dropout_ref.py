@@ -35,12 +35,10 @@ def threshold(p: float) -> int:
 
 
 def drop_hash(s32: np.uint32, x: np.ndarray) -> np.ndarray:
-    """Two multiply-xorshift rounds over uint32 (csrc/common.h drop_hash; first round (x + s32) * C1)."""
+    """Two multiply(-xorshift) rounds over uint32 (csrc/common.h drop_hash): ((x + s32) * C1 ^ >> 16) * C2."""
     h = ((x.astype(np.uint64) + np.uint64(s32)) & M32) * np.uint64(0x9E3779B1) & M32
     h ^= h >> np.uint64(16)
-    h = h * np.uint64(0x85EBCA6B) & M32
-    h ^= h >> np.uint64(13)
-    return h
+    return h * np.uint64(0x85EBCA6B) & M32
 
 
 def _keep(h: np.ndarray, half: np.ndarray, thr: int) -> np.ndarray:

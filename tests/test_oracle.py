@@ -112,8 +112,7 @@ def test_dropout_restatement():
     def h_py(s, x):
         h = (((x + s) & 0xFFFFFFFF) * 0x9E3779B1) & 0xFFFFFFFF
         h ^= h >> 16
-        h = (h * 0x85EBCA6B) & 0xFFFFFFFF
-        return h ^ (h >> 13)
+        return (h * 0x85EBCA6B) & 0xFFFFFFFF
 
     seed = 0x0123456789ABCDEF
     s32 = int(D.seed32(seed))
@@ -125,10 +124,12 @@ def test_dropout_restatement():
     # (adjacent keys, the next query row at T = 1024, the next 32-query half, the paired query q ^ 16)
     x = np.arange(1 << 20, dtype=np.uint64) * np.uint64(3) + np.uint64(977)
     keep = lambda idx, half: D._keep(D.drop_hash(np.uint32(s32), idx), np.full(idx.shape, half), 6554)  # noqa
-    base = keep(x, 0).astype(np.float64)
-    for stride, half in ((1, 0), (1024, 0), (32 * 1024, 0), (0, 1)):
-        other = keep(x + np.uint64(stride), half).astype(np.float64)
-        assert abs(float(np.corrcoef(base, other)[0, 1])) < 0.01, (stride, half)
+    for h0 in (0, 1):
+        base = keep(x, h0).astype(np.float64)
+        for stride, half in ((1, 0), (1, 1), (2, 0), (16, 1), (1024, 0), (1024, 1), (32 * 1024, 0), (1 << 16, 1),
+                             (0, 1 - h0)):
+            other = keep(x + np.uint64(stride), half).astype(np.float64)
+            assert abs(float(np.corrcoef(base, other)[0, 1])) < 0.01, (h0, stride, half)
     m = D.site_scale(seed, 256, 768, 0.1)
     assert abs(float((m == 0).float().mean()) - 0.1) < 0.005
     assert torch.allclose(m[m > 0], torch.tensor(1 / 0.9))
