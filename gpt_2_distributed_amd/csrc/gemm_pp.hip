@@ -485,7 +485,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
       for (int e = 0; e < 4; ++e) v[e] += bias[e];
       if constexpr (EPI == EPI_SLAB) {
         float* slab = reinterpret_cast<float*>(P.C) + (size_t)split * P.M * P.ldc;
-        *reinterpret_cast<f32x4*>(slab + (size_t)gm * P.ldc + gn) = v;
+        store4<float>(slab + (size_t)gm * P.ldc + gn, v);
       } else {
         constexpr int DROPM = (EPI == EPI_RESID || EPI == EPI_GELU) ? VC : -1;
         const f32x4 o = epilogue_apply<EPI, bf16, DROPM>(P, gm, gn, v, kOpnd ? opnd[it] : f32x4{0.f, 0.f, 0.f, 0.f});

@@ -114,6 +114,7 @@ def gemm_mode(libs, g, st):
         aux = torch.randn(Mt, n, device=dev, generator=g).to(torch.bfloat16) if epi in (K.EPI_GELU, K.EPI_GELU_BWD) else None
         data[name] = (lay, n, k, A, B, out, epi, bias, resid, aux)
     times = {(i, n): [] for i in range(len(libs)) for n in shapes}
+    stag = [int(v) for v in os.environ.get("LIB_AB_STAGGER", "").split(",") if v]
     ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
     ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
     for _ in range(5):
@@ -121,6 +122,8 @@ def gemm_mode(libs, g, st):
             ldb = k if lay == 0 else n
             pd = 0.1 if epi in (K.EPI_GELU, K.EPI_RESID) else 0.0
             for i, lib in enumerate(libs):
+                if stag:  # LIB_AB_STAGGER=0,12000: GPT2MI_PP_STAGGER per library (read per call)
+                    os.environ["GPT2MI_PP_STAGGER"] = str(stag[i])
                 fn = lambda: lib.gpt2mi_gemm(lay, epi, Mt, n, k, A.data_ptr(), k, B.data_ptr(), ldb,  # noqa: E731
                                              out.data_ptr(), n, ptr(bias), ptr(resid), ptr(aux), n if aux is not None else 0,
                                              1.0, None, 0, 1, pd, 5, None, st)
