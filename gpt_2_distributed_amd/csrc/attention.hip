@@ -155,7 +155,7 @@ __device__ __forceinline__ void attn_block(int& bh, int& blk) {
 
 // ---------------------------------------------------------------------------------------------
 template <bool DROP>
-__global__ __launch_bounds__(kThreads, DROP ? 4 : 3) void attn_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
+__global__ __launch_bounds__(kThreads, 3) void attn_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
                                                                float* __restrict__ lse, int T, int H, float scale,
                                                                uint64_t seed, uint32_t thr, float inv_keep) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * BKV * 128];  // 2 stages x (K, V)
@@ -262,28 +262,33 @@ __global__ __launch_bounds__(kThreads, DROP ? 4 : 3) void attn_fwd_kernel(const 
 #pragma unroll
           for (int r = 0; r < 4; ++r) s[qg][fi][r] = __builtin_amdgcn_exp2f(fmaf(s[qg][fi][r], sl2, -m[qg]));
       }
-      // row sums before dropout (the normaliser is the undropped softmax denominator)
+      // P packed to bf16 once per 32-key half (kk): the row sums (before dropout: the normaliser is the undropped
+      // softmax denominator) and P.V read the same fragments. Dropout on the packed P (its 1/(1-p) goes into the
+      // final scale): one hash per (q, q^16) pair of a key, both decisions from one packed int16 subtract.
+      [[maybe_unused]] uint32_t pre = 0, tk2 = 0;
+      if constexpr (DROP) {
+        pre = drop_pre(seed32(seed), ((uint32_t)bh * T + q_lo + (lane & 15)) * (uint32_t)T + k_lo + 4 * g);
+        tk2 = drop_tk2(thr);
+      }
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
-        o[0][4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pack_perm(s[0], kk), o[0][4], 0, 0, 0);
-        o[1][4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pack_perm(s[1], kk), o[1][4], 0, 0, 0);
-      }
-      if constexpr (DROP) {  // dropout on P (not on the normaliser; the 1/(1-p) goes into the final scale): one
-                  // hash per (q, q^16) pair of a key
-        const uint32_t s32 = seed32(seed);
-        const uint32_t pre = drop_pre(s32, ((uint32_t)bh * T + q_lo + (lane & 15)) * (uint32_t)T + k_lo + 4 * g);
+        bf16x8 p0 = pack_perm(s[0], kk), p1 = pack_perm(s[1], kk);
+        o[0][4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, p0, o[0][4], 0, 0, 0);
+        o[1][4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, p1, o[1][4], 0, 0, 0);
+        if constexpr (DROP) {
+          u32x4 w0 = __builtin_bit_cast(u32x4, p0), w1 = __builtin_bit_cast(u32x4, p1);
 #pragma unroll
-        for (int fi = 0; fi < 4; ++fi)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const uint32_t hh = drop_fin(pre + (uint32_t)(16 * fi + r) * kDropC1);
-            if (!drop_keep16(hh, 0, thr)) s[0][fi][r] = 0.f;
-            if (!drop_keep16(hh, 1, thr)) s[1][fi][r] = 0.f;
+          for (int d = 0; d < 4; ++d) {  // dword d: keys (fi, r), (fi, r + 1) with fi = 2kk + (d >> 1), r = 2(d & 1)
+            const uint32_t c = 16 * (2 * kk + (d >> 1)) + 2 * (d & 1);
+            const uint32_t ka = drop_keep_mask2(tk2, drop_fin(pre + c * kDropC1));
+            const uint32_t kb = drop_keep_mask2(tk2, drop_fin(pre + (c + 1) * kDropC1));
+            // the bytes of each bf16 = the sign (keep bit) of key r's / key r+1's decision for query group 0 / 1
+            w0[d] &= __builtin_amdgcn_perm(kb, ka, 0x0A0A0808u);
+            w1[d] &= __builtin_amdgcn_perm(kb, ka, 0x0B0B0909u);
           }
-      }
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const bf16x8 p0 = pack_perm(s[0], kk), p1 = pack_perm(s[1], kk);
+          p0 = __builtin_bit_cast(bf16x8, w0);
+          p1 = __builtin_bit_cast(bf16x8, w1);
+        }
 #pragma unroll
         for (int fd = 0; fd < 4; ++fd) {
           const bf16x8 vt = tr_frag(Vs, kk, 16 * fd, lane);

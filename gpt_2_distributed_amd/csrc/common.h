@@ -52,7 +52,7 @@ __device__ __forceinline__ float wave_max(float v) {
 // keep(i) is a pure function of (seed, element index), so backward regenerates the forward mask
 // without storing it. One 32-bit multiply-xorshift hash yields TWO 16-bit uniforms: element pairs
 // share a hash (GEMM/LN/embedding sites: elements 2j, 2j+1; attention: queries q, q^16 of one key,
-// which sit in the same lane in every attention kernel). keep = uniform16 >= round(p * 2^16).
+// which sit in the same lane in every attention kernel). keep = int16(uniform16) >= round(p * 2^16) - 2^15.
 // All element / pair indices fit in 32 bits for every BASELINE config (attention B*H*T*T < 2^32).
 __device__ __forceinline__ uint32_t seed32(uint64_t seed) { return (uint32_t)seed ^ (uint32_t)(seed >> 32); }
 // Two rounds of multiply-xorshift (murmur3 fmix32 without its closing rounds). The first round is linear in the
@@ -69,8 +69,23 @@ __device__ __forceinline__ uint32_t drop_fin(uint32_t h) {
   return h * kDropC2;
 }
 __device__ __forceinline__ uint32_t drop_hash(uint32_t s32, uint32_t x) { return drop_fin(drop_pre(s32, x)); }
+// keep iff the 16-bit half, read as a signed int16, is >= thr - 32768 (P(keep) = 1 - thr / 2^16): a signed
+// threshold, so packed-int16 arithmetic can form the decisions of a pair at once from the sign bits of
+// (thr - 32769) -sat- half (drop_keep_mask2)
 __device__ __forceinline__ bool drop_keep16(uint32_t h, int half, uint32_t thr) {
-  return ((half ? (h >> 16) : h) & 0xFFFFu) >= thr;
+  // h opaque (no instruction): otherwise sext(low half of x * C2) becomes a second multiply, by C2 << 16
+  asm("" : "+v"(h));
+  return (int)(int16_t)(half ? (h >> 16) : h) >= (int)thr - 32768;
+}
+// Both decisions of hash h at once, for the packed path: bit 15 / bit 31 of the result are set iff half 0 / 1
+// is kept. tk2 = drop_tk2(thr) (thr >= 1): (thr - 32769) in both int16 halves; saturation keeps the sign exact.
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+__host__ __device__ __forceinline__ uint32_t drop_tk2(uint32_t thr) {
+  const uint32_t t = (uint32_t)(uint16_t)(int16_t)((int)thr - 32769);
+  return t | (t << 16);
+}
+__device__ __forceinline__ uint32_t drop_keep_mask2(uint32_t tk2, uint32_t h) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(__builtin_bit_cast(s16x2, tk2), __builtin_bit_cast(s16x2, h)));
 }
 // element-indexed form: element i uses half (i & 1) of hash(i >> 1)
 __device__ __forceinline__ bool drop_keep(uint64_t seed, uint64_t idx, uint32_t thr) {

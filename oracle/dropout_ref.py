@@ -13,7 +13,8 @@ Element indexing per site (the kernels' own):
     hash(seed, e >> 1), 16-bit half e & 1 (`csrc/norm_embed.hip`, `csrc/gemm_common.h`);
   * attention probabilities [B*H, T(q), T(key)]: hash(seed, (bh * T + (q & ~16)) * T + key), half
     (q >> 4) & 1 (`csrc/attention.hip`, `csrc/fp32.hip`).
-keep = uniform16 >= round(p * 2^16).
+keep = int16(uniform16) >= round(p * 2^16) - 2^15, i.e. (uniform16 ^ 0x8000) >= round(p * 2^16): P(keep) = 1 - p
+(a signed threshold, so the attention forward decides a pair with one packed int16 subtract).
 """
 from __future__ import annotations
 
@@ -42,7 +43,9 @@ def drop_hash(s32: np.uint32, x: np.ndarray) -> np.ndarray:
 
 
 def _keep(h: np.ndarray, half: np.ndarray, thr: int) -> np.ndarray:
-    return ((h >> (np.uint64(16) * half.astype(np.uint64))) & np.uint64(0xFFFF)) >= np.uint64(thr)
+    """drop_keep16 (csrc/common.h): the 16-bit half as int16 >= thr - 2^15."""
+    u = (h >> (np.uint64(16) * half.astype(np.uint64))) & np.uint64(0xFFFF)
+    return (u ^ np.uint64(0x8000)) >= np.uint64(thr)
 
 
 def site_scale(seed: int, rows: int, cols: int, p: float) -> torch.Tensor:

@@ -136,7 +136,8 @@ def test_dropout_restatement():
     # elements 2j, 2j+1 share hash j: halves 0 / 1
     e = np.arange(16, dtype=np.uint64)
     hv = D.drop_hash(D.seed32(seed), e >> np.uint64(1))
-    keep = ((hv >> (np.uint64(16) * (e & np.uint64(1)))) & np.uint64(0xFFFF)) >= 6554
+    half16 = (hv >> (np.uint64(16) * (e & np.uint64(1)))) & np.uint64(0xFFFF)
+    keep = half16.astype(np.uint16).view(np.int16).astype(np.int64) >= 6554 - 32768  # signed threshold
     assert np.array_equal(keep, (m.reshape(-1)[:16] > 0).numpy())
     a = D.attn_scale(seed, 2, 64, 0.1)
     assert abs(float((a == 0).float().mean()) - 0.1) < 0.01
@@ -144,8 +145,9 @@ def test_dropout_restatement():
     q, k = 3, 40
     x = (1 * 64 + (q & ~16)) * 64 + k
     hh = h_py(s32, x)
-    assert (a[1, q, k] > 0).item() == ((hh & 0xFFFF) >= 6554)
-    assert (a[1, q ^ 16, k] > 0).item() == (((hh >> 16) & 0xFFFF) >= 6554)
+    s16 = lambda v: v - 65536 if v >= 32768 else v  # noqa: E731
+    assert (a[1, q, k] > 0).item() == (s16(hh & 0xFFFF) >= 6554 - 32768)
+    assert (a[1, q ^ 16, k] > 0).item() == (s16((hh >> 16) & 0xFFFF) >= 6554 - 32768)
     params = model_ref.init_params(TINY)
     idx = torch.randint(0, 509, (2, 64), generator=torch.Generator().manual_seed(1))
     ones = {kk: torch.ones_like(v) for kk, v in D.step_masks({"embd": 1, **{(s, l): 1 for s in ("attn", "proj", "fc1", "fc2") for l in range(2)}}, 2, 64, 128, 2, 2, 0.1, 0.1).items()}

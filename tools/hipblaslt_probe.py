@@ -45,3 +45,16 @@ for name, m, n, k in shapes:
     f = 2.0 * m * n * k
     print(f"{name:18s} hipBLASLt {t_blt:7.3f} ms {f / t_blt / 1e9:6.0f} TF | libgpt2mi {t_own:7.3f} ms {f / t_own / 1e9:6.0f} TF")
     del a, w, out
+
+# weight gradients dW[m_out, n_in] = dY^T . X over K = M tokens (both operands token-major: the transposed layout)
+for name, mo, ni in (("lm_head wgrad", Vp, C), ("qkv wgrad", 3 * C, C), ("fc1 wgrad", 4 * C, C), ("fc2 wgrad", C, 4 * C)):
+    dy, x = r(M, mo), r(M, ni)
+    out = torch.empty(mo, ni, dtype=torch.bfloat16, device=dev)
+    t_blt = timeit(lambda: torch.mm(dy.t(), x, out=out))
+    sp = K.wgrad_splits(mo, ni, M)
+    ws = torch.empty(sp * mo * ni, device=dev)
+    acc = torch.zeros(mo, ni, device=dev)
+    t_own = timeit(lambda: K.gemm_wgrad(mo, ni, M, dy, mo, x, ni, acc, ni, True, 1.0, None, ws, sp))
+    f = 2.0 * M * mo * ni
+    print(f"{name:18s} hipBLASLt {t_blt:7.3f} ms {f / t_blt / 1e9:6.0f} TF | libgpt2mi {t_own:7.3f} ms {f / t_own / 1e9:6.0f} TF")
+    del dy, x, out, ws, acc
