@@ -249,7 +249,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   const int kbeg = split * P.k_per_split;
   const int nk = (min(P.K, kbeg + P.k_per_split) - kbeg) / BK;  // even (host-checked)
 
-  // PERSIST: vector-memory stores each wave issues in an epilogue (one per output row and output array)
+  // PERSIST: vector-memory stores each wave issues in an epilogue (one per output row and output array; the
+  // column-sum atomic of waves 0-3 only makes the waits below retire more, never less)
   constexpr int kStores = EPI == EPI_GELU ? 64 : 32;
   bool after_epi = false;  // the current tile follows an epilogue (wave-uniform)
   f32x4 acc[2][2][4][2];
@@ -361,7 +362,15 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   __builtin_amdgcn_sched_barrier(0);
   PP_STAMP(2)
 
-  const int tid = threadIdx.x;
+  // the thread index through an opaque copy: lane constants derived from it are formed here, per tile, instead of
+  // being hoisted to kernel entry and spilled across the tile loop (whose reloads would wait vmcnt(0) behind the
+  // next tile's DMAs)
+  int tid = threadIdx.x;
+  if constexpr (PERSIST) {  // wave id (SGPR) * 64 + the lane id recomputed by v_mbcnt (no VGPR kept live for it)
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    tid = wid * 64 + l;
+  }
   const int ch = tid & 63;
   const int gn = n0 + 4 * ch;
   const f32x4 bias = (P.bias && EPI != EPI_GELU_BWD) ? *reinterpret_cast<const f32x4*>(P.bias + gn)
@@ -392,17 +401,33 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   // [128][256] fp32 image (1 KiB rows) over the whole LDS; PERSIST: [64][256] in buffer 1
   float* img = reinterpret_cast<float*>(PERSIST ? buf1 : smem);
   constexpr bool kOpnd = EPI == EPI_RESID || EPI == EPI_GELU_BWD || EPI == EPI_F32;
-  // fused bias grad of the stored output (never selected with the persistent schedule)
-  constexpr bool kCsum = !PERSIST && (EPI == EPI_BF16 || EPI == EPI_GELU_BWD);
+  // fused bias grad of the stored output (column sums of the rounded stores; reduced per tile below; the
+  // persistent schedule has the registers for it only beside the GELU_BWD epilogue, the one that uses it)
+  constexpr bool kCsum = PERSIST ? EPI == EPI_GELU_BWD : (EPI == EPI_BF16 || EPI == EPI_GELU_BWD);
   const bool csum_on = kCsum && P.dbias != nullptr;
-  f32x4 csum = {0.f, 0.f, 0.f, 0.f};
+  f32x4 csum;
+  if constexpr (PERSIST) {  // formed per tile (a zero vector hoisted out of the tile loop got spilled)
+    float z;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+    csum = f32x4{z, z, z, z};
+  } else {
+    csum = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   if constexpr (PERSIST) {
     // four 64-row passes: pass q = 2*mi + g holds rows q*64.. (the 16-row groups of waves with wr == g)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int mi = q >> 1, g = q & 1;
-      f32x4 opnd[8];
-      if constexpr (kOpnd) {
+      // the pass's epilogue operands, in flight while the accumulators go through LDS (the bf16 GELU derivative
+      // held as loaded: 2 VGPRs a row instead of 4)
+      [[maybe_unused]] f32x4 opnd[8];
+      [[maybe_unused]] bf16x4 opnd16[8];
+      if constexpr (EPI == EPI_GELU_BWD) {
+#pragma unroll
+        for (int it = 0; it < 8; ++it)
+          opnd16[it] = *reinterpret_cast<const bf16x4*>(reinterpret_cast<const bf16*>(P.aux) +
+                                                        (size_t)(m0 + q * 64 + it * 8 + wid) * P.ldaux + gn);
+      } else if constexpr (kOpnd) {
 #pragma unroll
         for (int it = 0; it < 8; ++it) opnd[it] = epilogue_operand<EPI>(P, min(m0 + q * 64 + it * 8 + wid, P.M - 1), gn);
       }
@@ -429,18 +454,29 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
         const int r = it * 8 + wid;
         v[it] = *reinterpret_cast<const f32x4*>(img + r * 256 + 4 * (ch ^ (r & 15)));
       }
-      // every row exists (M % 256 == 0, host-checked) and dropout is decided once per pass: straight-line rows
-      auto rows = [&](auto drop_c) {
+      // every row exists (M % 256 == 0, host-checked); the per-tile switch (dropout for RESID / GELU, the fused
+      // column sums for BF16 / GELU_BWD) is decided once per pass: straight-line rows
+      auto rows = [&](auto vc) {
+        constexpr int VC = decltype(vc)::value;
 #pragma unroll
         for (int it = 0; it < 8; ++it) {
           const int gm = m0 + q * 64 + it * 8 + wid;
           f32x4 w = v[it];
 #pragma unroll
           for (int e = 0; e < 4; ++e) w[e] += bias[e];
-          epilogue_apply<EPI, bf16, decltype(drop_c)::value>(P, gm, gn, w, kOpnd ? opnd[it] : f32x4{0.f, 0.f, 0.f, 0.f});
+          f32x4 op = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (EPI == EPI_GELU_BWD) op = f32x4{bf2f(opnd16[it][0]), bf2f(opnd16[it][1]), bf2f(opnd16[it][2]),
+                                                         bf2f(opnd16[it][3])};
+          else if constexpr (kOpnd) op = opnd[it];
+          const f32x4 o = epilogue_apply<EPI, bf16, (EPI == EPI_RESID || EPI == EPI_GELU) ? VC : 0>(P, gm, gn, w, op);
+          if constexpr (kCsum && VC == 1) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) csum[e] += o[e];
+          }
         }
       };
-      if (P.thr) rows(std::integral_constant<int, 1>{});
+      const bool on = (EPI == EPI_RESID || EPI == EPI_GELU) ? P.thr != 0u : csum_on;
+      if (on) rows(std::integral_constant<int, 1>{});
       else rows(std::integral_constant<int, 0>{});
     }
   } else {
@@ -592,6 +628,11 @@ int launch_persistent(const GemmParams& P, hipStream_t s) {
 }  // namespace
 
 namespace gpt2mi {
+#ifndef GPT2MI_PERSIST_KMAX
+#define GPT2MI_PERSIST_KMAX 1024
+#endif
+// longest K that takes the persistent schedule by default (a tile's epilogue is a smaller share past it)
+constexpr int g_persist_kmax = GPT2MI_PERSIST_KMAX;
 // Layouts 0 / 1; N % 256 == 0, every split's K range an even number (>= 2) of 64-deep tiles.
 // Returns -1 when this kernel does not apply (the caller falls back).
 int gemm_pp_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t s, int splits, int map) {
@@ -615,15 +656,22 @@ int gemm_pp_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t 
       if (map == 3) return launch<false, true, EPI_BF16, 3>(P, s, 1);
     }
   }
-  // short-K forward-layout shapes with no epilogue operand loads: the persistent schedule (map < 0 forces
-  // the one-tile-per-block kernel, map 7 the persistent one at any K: tools/gemm_ab.py)
+  // short-K forward-layout shapes: the persistent schedule (map < 0 forces the one-tile-per-block kernel, map 7
+  // the persistent one at any K: tools/gemm_ab.py). Epilogue operand loads (residual, GELU derivative) are
+  // issued after the next tile's asm DMAs, so the compiler's wait for them retires those DMAs too — early,
+  // never late.
   const int ntiles = ((P.M + BM - 1) / BM) * (P.N / BN);
-  if (layout == 0 && (map == 7 || (map == 0 && g_gemm_persistent && P.K <= 1024)) && P.K >= 4 * BK &&
+  if (layout == 0 && (map == 7 || (map == 0 && g_gemm_persistent && P.K <= g_persist_kmax)) && P.K >= 4 * BK &&
       ntiles >= 2 * num_cus() &&
-      P.dbias == nullptr &&
-      (epilogue == EPI_BF16 || epilogue == EPI_GELU) && P.M % BM == 0 && (size_t)P.M * P.lda * 2 < (1ull << 31) &&
-      (size_t)P.N * P.ldb * 2 < (1ull << 31)) {
-    return epilogue == EPI_BF16 ? launch_persistent<EPI_BF16>(P, s) : launch_persistent<EPI_GELU>(P, s);
+      ((epilogue == EPI_BF16 && P.dbias == nullptr) || epilogue == EPI_GELU || epilogue == EPI_RESID ||
+       epilogue == EPI_GELU_BWD) &&
+      P.M % BM == 0 && (size_t)P.M * P.lda * 2 < (1ull << 31) && (size_t)P.N * P.ldb * 2 < (1ull << 31)) {
+    switch (epilogue) {
+      case EPI_BF16: return launch_persistent<EPI_BF16>(P, s);
+      case EPI_GELU: return launch_persistent<EPI_GELU>(P, s);
+      case EPI_RESID: return launch_persistent<EPI_RESID>(P, s);
+      default: return launch_persistent<EPI_GELU_BWD>(P, s);
+    }
   }
   if (map < 0 || map == 7) map = 0;
   switch (layout * 16 + epilogue) {

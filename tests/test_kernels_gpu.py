@@ -506,29 +506,41 @@ def test_transpose_bf16_batched():
         assert torch.all(dst[off + r * c:off + r * c + 64] == 7.0)
 
 
-@pytest.mark.parametrize("epi", ["plain", "bias", "gelu_drop"])
-@pytest.mark.parametrize("M,N", [(8192, 4096), (65536, 2304)])
+@pytest.mark.parametrize("epi", ["plain", "bias", "gelu_drop", "resid_drop", "gelu_bwd_dbias"])
+@pytest.mark.parametrize("M,N", [(8192, 4096), (65536, 2304), (65536, 768)])
 def test_gemm_persistent_schedule_bitwise(epi, M, N):
     """The persistent ping-pong schedule (short-K forward-layout GEMMs with >= 2 tiles per CU: one block per CU
     walks the tiles, the next tile's first K-tile lands during this tile's epilogue) computes every output
     element exactly as the one-tile-per-block kernel (gpt2mi_set_gemm_impl(6) forces that one): bitwise equal,
-    and within bf16 rounding of an fp32 reference on sampled rows."""
+    and within bf16 rounding of an fp32 reference on sampled rows. Covers every epilogue the step runs on it:
+    plain / bias (qkv, proj dgrad), GELU + dropout (fc1), fp32 residual + dropout (proj forward) and the GELU
+    derivative product with its fused bias gradient (fc2 dgrad; column sums by atomics, so to fp32 rounding)."""
     K = 768
     g = torch.Generator().manual_seed(M + N)
     A = bf(torch.randn(M, K, generator=g)).to(dev)
     W = bf(torch.randn(N, K, generator=g) * 0.05).to(dev)
-    bias = torch.randn(N, generator=g).to(dev) if epi != "plain" else None
-    outs = []
+    bias = torch.randn(N, generator=g).to(dev) if epi not in ("plain", "gelu_bwd_dbias") else None
+    resid = torch.randn(M, N, generator=g).to(dev) if epi == "resid_drop" else None
+    dgelu = bf(torch.rand(M, N, generator=g) * 1.2 - 0.1).to(dev) if epi == "gelu_bwd_dbias" else None
+    outs, dbs = [], []
     for impl, persistent in ((0, True), (6, True), (0, False)):  # (0, False): the wrappers' no-persistent switch
         L().set_gemm_impl(impl)
         L().set_gemm_persistent(persistent)
         try:
-            C = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+            C = torch.empty(M, N, dtype=torch.float32 if epi == "resid_drop" else torch.bfloat16, device=dev)
             if epi == "gelu_drop":
                 aux = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
                 L().gemm(0, L().EPI_GELU, M, N, K, A, K, W, K, C, N, bias=bias, aux=aux, ldaux=N, p_drop=0.1,
                          seed=99)
                 outs.append((C, aux))
+            elif epi == "resid_drop":
+                L().gemm(0, L().EPI_RESID, M, N, K, A, K, W, K, C, N, bias=bias, resid=resid, p_drop=0.1, seed=98)
+                outs.append((C,))
+            elif epi == "gelu_bwd_dbias":
+                db = torch.zeros(N, device=dev)
+                L().gemm(0, L().EPI_GELU_BWD, M, N, K, A, K, W, K, C, N, aux=dgelu, ldaux=N, dbias=db)
+                outs.append((C,))
+                dbs.append(db)
             else:
                 L().gemm(0, L().EPI_BF16, M, N, K, A, K, W, K, C, N, bias=bias)
                 outs.append((C,))
@@ -541,8 +553,13 @@ def test_gemm_persistent_schedule_bitwise(epi, M, N):
             assert torch.equal(a, b)
     rows = torch.arange(0, M, M // 64, device=dev)
     ref = A[rows].float() @ W.float().t() + (bias if bias is not None else 0.0)
-    if epi != "gelu_drop":
+    if epi in ("plain", "bias"):
         assert rel_err(outs[0][0][rows].float().cpu(), ref.cpu()) < 4e-3
+    if epi == "gelu_bwd_dbias":
+        assert rel_err(outs[0][0][rows].float().cpu(), (ref * dgelu[rows].float()).cpu()) < 4e-3
+        full = outs[0][0].float().sum(0)  # the bias grad = column sums of the stored (bf16-rounded) output
+        for db in dbs:
+            assert torch.allclose(db, full, rtol=1e-4, atol=1e-3 * full.abs().max().item())
 
 
 @pytest.mark.parametrize("m,n,tokens,splits", [(2304, 768, 8192, 4), (768, 3072, 8192, 8), (50432, 768, 4096, 3)])

@@ -113,10 +113,30 @@ def gemm_mode(libs, g, st):
         resid = torch.randn(Mt, n, device=dev, generator=g) if epi == K.EPI_RESID else None
         aux = torch.randn(Mt, n, device=dev, generator=g).to(torch.bfloat16) if epi in (K.EPI_GELU, K.EPI_GELU_BWD) else None
         data[name] = (lay, n, k, A, B, out, epi, bias, resid, aux)
+    # outputs of every library vs the first: C bitwise, the fused bias grad (atomics: any order) to 1e-5
+    ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+    for name, (lay, n, k, A, B, out, epi, bias, resid, aux) in data.items():
+        ref = None
+        for i, lib in enumerate(libs):
+            o = torch.empty_like(out)
+            db = torch.zeros(n, device=dev) if epi == K.EPI_GELU_BWD else None
+            pd = 0.1 if epi in (K.EPI_GELU, K.EPI_RESID) else 0.0
+            a2 = aux.clone() if aux is not None else None
+            assert lib.gpt2mi_gemm(lay, epi, Mt, n, k, A.data_ptr(), k, B.data_ptr(), k if lay == 0 else n, o.data_ptr(),
+                                   n, ptr(bias), ptr(resid), ptr(a2), n if aux is not None else 0, 1.0, None, 0, 1, pd,
+                                   5, ptr(db), st) == 0
+            torch.cuda.synchronize()
+            if ref is None:
+                ref = (o, a2, db)
+                continue
+            if not torch.equal(o, ref[0]) or (a2 is not None and not torch.equal(a2, ref[1])):
+                print(f"MISMATCH lib{i} {name}", flush=True)
+            if db is not None and not torch.allclose(db, ref[2], rtol=1e-5, atol=1e-5):
+                print(f"MISMATCH lib{i} {name} dbias: {(db - ref[2]).abs().max().item()}", flush=True)
     times = {(i, n): [] for i in range(len(libs)) for n in shapes}
     stag = [int(v) for v in os.environ.get("LIB_AB_STAGGER", "").split(",") if v]
     ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
-    ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+    dbs = {name: torch.zeros(v[1], device=dev) for name, v in data.items() if v[6] == K.EPI_GELU_BWD}
     for _ in range(5):
         for name, (lay, n, k, A, B, out, epi, bias, resid, aux) in data.items():
             ldb = k if lay == 0 else n
@@ -126,7 +146,7 @@ def gemm_mode(libs, g, st):
                     os.environ["GPT2MI_PP_STAGGER"] = str(stag[i])
                 fn = lambda: lib.gpt2mi_gemm(lay, epi, Mt, n, k, A.data_ptr(), k, B.data_ptr(), ldb,  # noqa: E731
                                              out.data_ptr(), n, ptr(bias), ptr(resid), ptr(aux), n if aux is not None else 0,
-                                             1.0, None, 0, 1, pd, 5, None, st)
+                                             1.0, None, 0, 1, pd, 5, ptr(dbs.get(name)), st)
                 assert fn() == 0
                 s, e = ev(), ev()
                 s.record()
