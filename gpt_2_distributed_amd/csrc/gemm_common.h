@@ -169,6 +169,52 @@ __device__ __forceinline__ f32x4 epilogue_apply(const GemmParams& P, int gm, int
   return v;
 }
 
+// The bf16-output epilogues (BF16, GELU, GELU_BWD) on 8 consecutive outputs C[gm][gn..gn+7] (v0: gn..gn+3,
+// v1: gn+4..gn+7; op: the GELU_BWD operand as loaded), every output array written by ONE 16-B store per lane: the
+// epilogue's store tail is store-issue bound (per instruction, not per byte; cdna_hip_programming.md T21), so
+// half the instructions of the 4-wide form for the same bytes. Bitwise the same results as epilogue_apply.
+// r0 / r1: the primary output as stored (bf16-rounded), for fused column sums.
+__device__ __forceinline__ void store8_bf16(bf16* p, f32x4 a, f32x4 b) {
+  __builtin_nontemporal_store(bf16x8{f2bf(a[0]), f2bf(a[1]), f2bf(a[2]), f2bf(a[3]), f2bf(b[0]), f2bf(b[1]), f2bf(b[2]),
+                                     f2bf(b[3])},
+                              reinterpret_cast<bf16x8*>(p));
+}
+template <int EPI, int DROPM = -1>
+__device__ __forceinline__ void epilogue8(const GemmParams& P, int gm, int gn, f32x4 v0, f32x4 v1, bf16x8 op, f32x4& r0,
+                                          f32x4& r1) {
+  static_assert(EPI == EPI_BF16 || EPI == EPI_GELU || EPI == EPI_GELU_BWD, "bf16-output epilogues only");
+  const bool drop = DROPM < 0 ? P.thr != 0u : DROPM == 1;
+  bf16* C = reinterpret_cast<bf16*>(P.C) + (size_t)gm * P.ldc + gn;
+  if constexpr (EPI == EPI_BF16) {
+    store8_bf16(C, v0, v1);
+    r0 = round4<bf16>(v0);
+    r1 = round4<bf16>(v1);
+  } else if constexpr (EPI == EPI_GELU) {
+    const uint32_t pidx = (uint32_t)gm * (uint32_t)(P.N >> 1) + (uint32_t)(gn >> 1);
+    f32x4 h0, d0, h1, d1, m0 = {1.f, 1.f, 1.f, 1.f}, m1 = {1.f, 1.f, 1.f, 1.f};
+    if (drop) {
+      m0 = drop_scale4(P, pidx);
+      m1 = drop_scale4(P, pidx + 2);
+    }
+    gelu4(v0, m0, h0, d0);
+    gelu4(v1, m1, h1, d1);
+    store8_bf16(reinterpret_cast<bf16*>(P.aux) + (size_t)gm * P.ldaux + gn, d0, d1);
+    store8_bf16(C, h0, h1);
+    r0 = h0;
+    r1 = h1;
+  } else {
+    f32x4 o0, o1;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      o0[j] = v0[j] * bf2f(op[j]);
+      o1[j] = v1[j] * bf2f(op[4 + j]);
+    }
+    store8_bf16(C, o0, o1);
+    r0 = round4<bf16>(o0);
+    r1 = round4<bf16>(o1);
+  }
+}
+
 template <int EPI, typename TE = bf16>
 __device__ __forceinline__ void epilogue_store(const GemmParams& P, int gm, int gn, f32x4 v) {
   epilogue_apply<EPI, TE>(P, gm, gn, v, epilogue_operand<EPI, TE>(P, gm, gn));

@@ -251,7 +251,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
 
   // PERSIST: vector-memory stores each wave issues in an epilogue (one per output row and output array; the
   // column-sum atomic of waves 0-3 only makes the waits below retire more, never less)
-  constexpr int kStores = EPI == EPI_GELU ? 64 : 32;
+  // (bf16 outputs: one 16-B store per lane and row pair, so half as many)
+  constexpr bool kWide = !AIL && (EPI == EPI_BF16 || EPI == EPI_GELU || EPI == EPI_GELU_BWD);
+  constexpr int kStores = (EPI == EPI_GELU ? 64 : 32) / (kWide ? 2 : 1);
   bool after_epi = false;  // the current tile follows an epilogue (wave-uniform)
   f32x4 acc[2][2][4][2];
   auto zero_acc = [&]() {
@@ -373,8 +375,16 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   }
   const int ch = tid & 63;
   const int gn = n0 + 4 * ch;
-  const f32x4 bias = (P.bias && EPI != EPI_GELU_BWD) ? *reinterpret_cast<const f32x4*>(P.bias + gn)
-                                                     : f32x4{0.f, 0.f, 0.f, 0.f};
+  // bf16 outputs (kWide): lane (half hl, column group cj) owns columns 8cj..8cj+7 of the even / odd row of a pair
+  // (one 16-B store per row pair and output array); otherwise columns 4ch..4ch+3 of one row
+  const int cj = tid & 31, hl = (tid >> 5) & 1;
+  const int gnb = kWide ? n0 + 8 * cj : gn;  // first bias column of the lane
+  const bool has_bias = P.bias && EPI != EPI_GELU_BWD;
+  const f32x4 bias = has_bias ? *reinterpret_cast<const f32x4*>(P.bias + gnb) : f32x4{0.f, 0.f, 0.f, 0.f};
+  [[maybe_unused]] f32x4 bias1 = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (kWide) {
+    if (has_bias) bias1 = *reinterpret_cast<const f32x4*>(P.bias + gnb + 4);
+  }
   // PERSIST: the next tile's K-tile 0 goes into buffer 0 now (last read in this tile's final even K-tile,
   // several barriers ago); the epilogue image lives in buffer 1. The bias is waited for first: hipcc waits
   // vmcnt(0) at the first use of an ordinary load while an LDS-DMA is in flight, which would drain the
@@ -384,6 +394,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   bool has_next = false;
   if constexpr (PERSIST) {
     asm volatile("" ::"v"(bias[0]), "v"(bias[1]), "v"(bias[2]), "v"(bias[3]));
+    if constexpr (kWide) asm volatile("" ::"v"(bias1[0]), "v"(bias1[1]), "v"(bias1[2]), "v"(bias1[3]));
     vid += gridDim.x;
     has_next = vid < ntiles;
     if (has_next) {
@@ -406,14 +417,82 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   constexpr bool kCsum = PERSIST ? EPI == EPI_GELU_BWD : (EPI == EPI_BF16 || EPI == EPI_GELU_BWD);
   const bool csum_on = kCsum && P.dbias != nullptr;
   f32x4 csum;
+  [[maybe_unused]] f32x4 csum1;
   if constexpr (PERSIST) {  // formed per tile (a zero vector hoisted out of the tile loop got spilled)
     float z;
     asm volatile("v_mov_b32 %0, 0" : "=v"(z));
     csum = f32x4{z, z, z, z};
+    csum1 = csum;
   } else {
     csum = f32x4{0.f, 0.f, 0.f, 0.f};
+    csum1 = csum;
   }
-  if constexpr (PERSIST) {
+  if constexpr (kWide && PERSIST) {
+    // four 64-row passes as below; wave wid, half hl reads rows 16it + 2wid + hl (it = 0..3) of the pass's image,
+    // columns 8cj..8cj+7 (two 16-B chunks), and stores each output row pair with one 16-B store per lane
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int mi = q >> 1, g = q & 1;
+      [[maybe_unused]] bf16x8 op8[4];
+      if constexpr (EPI == EPI_GELU_BWD) {
+#pragma unroll
+        for (int it = 0; it < 4; ++it)
+          op8[it] = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16*>(P.aux) +
+                                                     (size_t)(m0 + q * 64 + 16 * it + 2 * wid + hl) * P.ldaux + gnb);
+      }
+      if (q) lds_barrier();  // the previous pass's reads are done before this pass overwrites the image
+      if (wr == g) {
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const int r = 16 * i + (lane & 15);
+              const int c = ni * 32 + wc * 8 + 4 * j + (lane >> 4);
+              f32x4 v = acc[mi][ni][i][j];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] *= alpha;
+              *reinterpret_cast<f32x4*>(img + r * 256 + 4 * (c ^ (r & 15))) = v;
+            }
+      }
+      lds_barrier();
+      f32x4 va[4], vb[4];
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const int r = 16 * it + 2 * wid + hl;
+        va[it] = *reinterpret_cast<const f32x4*>(img + r * 256 + 4 * ((2 * cj) ^ (r & 15)));
+        vb[it] = *reinterpret_cast<const f32x4*>(img + r * 256 + 4 * ((2 * cj + 1) ^ (r & 15)));
+      }
+      auto rows = [&](auto vc) {
+        constexpr int VC = decltype(vc)::value;
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+          const int gm = m0 + q * 64 + 16 * it + 2 * wid + hl;
+          f32x4 w0 = va[it], w1 = vb[it];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            w0[e] += bias[e];
+            w1[e] += bias1[e];
+          }
+          f32x4 r0, r1;
+          bf16x8 op = {};
+          if constexpr (EPI == EPI_GELU_BWD) op = op8[it];
+          epilogue8<EPI, EPI == EPI_GELU ? VC : 0>(P, gm, gnb, w0, w1, op, r0, r1);
+          if constexpr (kCsum && VC == 1) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              csum[e] += r0[e];
+              csum1[e] += r1[e];
+            }
+          }
+        }
+      };
+      const bool on = EPI == EPI_GELU ? P.thr != 0u : csum_on;
+      if (on) rows(std::integral_constant<int, 1>{});
+      else rows(std::integral_constant<int, 0>{});
+    }
+  } else if constexpr (PERSIST) {
     // four 64-row passes: pass q = 2*mi + g holds rows q*64.. (the 16-row groups of waves with wr == g)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -478,6 +557,83 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
       const bool on = (EPI == EPI_RESID || EPI == EPI_GELU) ? P.thr != 0u : csum_on;
       if (on) rows(std::integral_constant<int, 1>{});
       else rows(std::integral_constant<int, 0>{});
+    }
+  } else if constexpr (kWide) {
+    // one-tile-per-block, bf16 outputs: two 128-row passes; wave wid, half hl takes rows 16it + 2wid + hl
+    // (it = 0..7) of the pass, columns 8cj..8cj+7, one 16-B store per row pair and output array
+    const bool full = m0 + BM <= P.M;  // block-uniform
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+      [[maybe_unused]] bf16x8 op8[8];
+      if constexpr (EPI == EPI_GELU_BWD) {
+#pragma unroll
+        for (int it = 0; it < 8; ++it)
+          op8[it] = *reinterpret_cast<const bf16x8*>(
+              reinterpret_cast<const bf16*>(P.aux) +
+              (size_t)min(m0 + mi * 128 + 16 * it + 2 * wid + hl, P.M - 1) * P.ldaux + gnb);
+      }
+      if (mi) lds_barrier();  // pass 0's reads are done before pass 1 overwrites the image
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int r = wr * 64 + 16 * i + (lane & 15);
+            const int c = BIL ? wc * 16 + ni * 8 + 4 * j + (lane >> 4) : ni * 32 + wc * 8 + 4 * j + (lane >> 4);
+            f32x4 v = acc[mi][ni][i][j];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] *= alpha;
+            *reinterpret_cast<f32x4*>(img + r * 256 + 4 * (c ^ (r & 15))) = v;
+          }
+      lds_barrier();
+      // VC: the per-tile switch (dropout for GELU, the fused column sums for BF16 / GELU_BWD); GUARD: partial
+      // tile. Two halves of 4 row pairs (their 16 image reads in flight together; 32 VGPRs live, not 64)
+      auto rows = [&](auto vc, auto guard_c) {
+        constexpr int VC = decltype(vc)::value;
+        constexpr bool GUARD = decltype(guard_c)::value;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+        f32x4 va[4], vb[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int r = 16 * (4 * half + k) + 2 * wid + hl;
+          va[k] = *reinterpret_cast<const f32x4*>(img + r * 256 + 4 * ((2 * cj) ^ (r & 15)));
+          vb[k] = *reinterpret_cast<const f32x4*>(img + r * 256 + 4 * ((2 * cj + 1) ^ (r & 15)));
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int it = 4 * half + k;
+          const int gm = m0 + mi * 128 + 16 * it + 2 * wid + hl;
+          if (GUARD && gm >= P.M) continue;
+          f32x4 w0 = va[k], w1 = vb[k];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            w0[e] += bias[e];
+            w1[e] += bias1[e];
+          }
+          f32x4 r0, r1;
+          bf16x8 op = {};
+          if constexpr (EPI == EPI_GELU_BWD) op = op8[it];
+          epilogue8<EPI, EPI == EPI_GELU ? VC : 0>(P, gm, gnb, w0, w1, op, r0, r1);
+          if constexpr (kCsum && VC == 1) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              csum[e] += r0[e];
+              csum1[e] += r1[e];
+            }
+          }
+        }
+        }
+      };
+      const bool on = EPI == EPI_GELU ? P.thr != 0u : csum_on;
+      if (full) {
+        if (on) rows(std::integral_constant<int, 1>{}, std::false_type{});
+        else rows(std::integral_constant<int, 0>{}, std::false_type{});
+      } else {
+        if (on) rows(std::integral_constant<int, 1>{}, std::true_type{});
+        else rows(std::integral_constant<int, 0>{}, std::true_type{});
+      }
     }
   } else {
 #pragma unroll
@@ -559,7 +715,19 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   if constexpr (kCsum) {
     if (csum_on) {  // the 8 waves hold partial sums of the same 256 columns: reduce in LDS, 1 atomic/column
       lds_barrier();  // every wave has finished reading the staging image
-      *reinterpret_cast<f32x4*>(img + (tid >> 6) * 256 + 4 * ch) = csum;
+      if constexpr (kWide) {  // lanes l and l ^ 32 hold the same 8 columns (even / odd rows)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          csum[e] += __shfl_xor(csum[e], 32);
+          csum1[e] += __shfl_xor(csum1[e], 32);
+        }
+        if (hl == 0) {
+          *reinterpret_cast<f32x4*>(img + wid * 256 + 8 * cj) = csum;
+          *reinterpret_cast<f32x4*>(img + wid * 256 + 8 * cj + 4) = csum1;
+        }
+      } else {
+        *reinterpret_cast<f32x4*>(img + (tid >> 6) * 256 + 4 * ch) = csum;
+      }
       lds_barrier();
       if (tid < 256) {
         float t = 0.f;
