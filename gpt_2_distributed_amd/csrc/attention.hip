@@ -99,6 +99,26 @@ __device__ __forceinline__ float tile_colsum(const f32x4 (&v)[2][4], float scale
 }
 __device__ __forceinline__ int tile_colsum_col(int lane) { return 16 * ((lane & 15) >> 2) + 4 * (lane >> 4) + (lane & 3); }
 
+// One 64-wide output row (head_dim) of a wave's MFMA accumulators, v[fd][r] = row value at d = 16fd + 4g + r
+// (g = lane >> 4), scaled by sc and stored as bf16 with two 16-B stores per lane instead of four 8-B ones (the
+// output tail is store-issue bound; cdna_hip_programming.md T21): a permlane16 swap per dword hands lane group g
+// the 8 contiguous d of the pair (fd, fd + 1) it stores — d 16(g & 1) + 8(g >> 1) .. +8 of the pair's 32.
+__device__ __forceinline__ void store_row64(bf16* row, const f32x4 (&v)[4], float sc, int lane) {
+  const int g = lane >> 4;
+#pragma unroll
+  for (int pr = 0; pr < 2; ++pr) {
+    const bf16x4 a = {f2bf(v[2 * pr][0] * sc), f2bf(v[2 * pr][1] * sc), f2bf(v[2 * pr][2] * sc), f2bf(v[2 * pr][3] * sc)};
+    const bf16x4 b = {f2bf(v[2 * pr + 1][0] * sc), f2bf(v[2 * pr + 1][1] * sc), f2bf(v[2 * pr + 1][2] * sc),
+                      f2bf(v[2 * pr + 1][3] * sc)};
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    const u32x2 ua = __builtin_bit_cast(u32x2, a), ub = __builtin_bit_cast(u32x2, b);
+    // rows 1 / 3 of the first operand <-> rows 0 / 2 of the second
+    const auto x = __builtin_amdgcn_permlane16_swap(ua[0], ub[0], false, false);
+    const auto y = __builtin_amdgcn_permlane16_swap(ua[1], ub[1], false, false);
+    *reinterpret_cast<u32x4*>(row + 32 * pr + 16 * (g & 1) + 8 * (g >> 1)) = u32x4{x[0], y[0], x[1], y[1]};
+  }
+}
+
 constexpr float kRescaleThr = 8.f;  // log2 units: P <= 256 between rescales (bf16-exact exponent range)
 
 // pack accumulator registers acc[2kk + (j>>2)][j&3] (j = 0..7) to a bf16 operand fragment
@@ -305,11 +325,8 @@ __global__ __launch_bounds__(kThreads, 3) void attn_fwd_kernel(const bf16* __res
     const int q = q_lo + 16 * qg + (lane & 15);
     const float lq = o[qg][4][0];
     const float il = (DROP ? inv_keep : 1.f) / lq;
-    bf16* op = out + ((size_t)b * T + q) * C + h * D;
-#pragma unroll
-    for (int fd = 0; fd < 4; ++fd)
-      *reinterpret_cast<bf16x4*>(op + 16 * fd + 4 * g) = bf16x4{f2bf(o[qg][fd][0] * il), f2bf(o[qg][fd][1] * il),
-                                                                f2bf(o[qg][fd][2] * il), f2bf(o[qg][fd][3] * il)};
+    const f32x4 ov[4] = {o[qg][0], o[qg][1], o[qg][2], o[qg][3]};
+    store_row64(out + ((size_t)b * T + q) * C + h * D, ov, il, lane);
     if (g == 0) lse[(size_t)bh * T + q] = (m[qg] + log2f(lq)) / kLog2e;  // natural-log LSE of scaled scores
   }
 }
@@ -444,12 +461,8 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const bf16* __
 #pragma unroll
   for (int qg = 0; qg < 2; ++qg) {
     const int q = q_lo + 16 * qg + (lane & 15);
-    bf16* dp_out = dqkv + ((size_t)b * T + q) * ld + h * D;
-#pragma unroll
-    for (int fd = 0; fd < 4; ++fd)
-      *reinterpret_cast<bf16x4*>(dp_out + 16 * fd + 4 * g) =
-          bf16x4{f2bf(dq[qg][fd][0] * scale), f2bf(dq[qg][fd][1] * scale), f2bf(dq[qg][fd][2] * scale),
-                 f2bf(dq[qg][fd][3] * scale)};
+    const f32x4 qv[4] = {dq[qg][0], dq[qg][1], dq[qg][2], dq[qg][3]};
+    store_row64(dqkv + ((size_t)b * T + q) * ld + h * D, qv, scale, lane);
   }
   if (csum) {  // partial qkv-bias gradient: row (b*T + q_lo)/32 of csum [B*T/32][3C], q columns
     const float cs = tile_colsum(dq, scale, lane);
@@ -614,17 +627,10 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dkdv_kernel(const bf16* 
   for (int kg = 0; kg < 2; ++kg) {
     const int key = k_lo + 16 * kg + (lane & 15);
     bf16* kout = dqkv + ((size_t)b * T + key) * ld + C + h * D;
-    bf16* vout = kout + C;
-#pragma unroll
-    for (int fd = 0; fd < 4; ++fd) {
-      *reinterpret_cast<bf16x4*>(kout + 16 * fd + 4 * g) =
-          bf16x4{f2bf(dk[kg][fd][0] * scale), f2bf(dk[kg][fd][1] * scale), f2bf(dk[kg][fd][2] * scale),
-                 f2bf(dk[kg][fd][3] * scale)};
-      const float vs = DROP ? inv_keep : 1.f;
-      *reinterpret_cast<bf16x4*>(vout + 16 * fd + 4 * g) =
-          bf16x4{f2bf(dv[kg][fd][0] * vs), f2bf(dv[kg][fd][1] * vs), f2bf(dv[kg][fd][2] * vs),
-                 f2bf(dv[kg][fd][3] * vs)};
-    }
+    const f32x4 kv[4] = {dk[kg][0], dk[kg][1], dk[kg][2], dk[kg][3]};
+    const f32x4 vv[4] = {dv[kg][0], dv[kg][1], dv[kg][2], dv[kg][3]};
+    store_row64(kout, kv, scale, lane);
+    store_row64(kout + C, vv, DROP ? inv_keep : 1.f, lane);
   }
   if (csum) {  // partial qkv-bias gradient: row (b*T + k_lo)/32 of csum [B*T/32][3C], k and v columns
     float* crow = csum + ((size_t)b * T + k_lo) / 32 * 3 * C + C + h * D + tile_colsum_col(lane);
