@@ -232,11 +232,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
                                                     float grad_scale, float* __restrict__ partials) {
   float sq = 0.f;
   const float decay = 1.f - lr * wd;
-  for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
-    f32x4 pv = reinterpret_cast<f32x4*>(p)[i];
-    f32x4 gv = reinterpret_cast<const f32x4*>(g)[i];
-    f32x4 mv = reinterpret_cast<f32x4*>(m)[i];
-    f32x4 vv = reinterpret_cast<f32x4*>(v)[i];
+  auto upd = [&](f32x4& pv, f32x4 gv, f32x4& mv, f32x4& vv) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const float gg = gv[j] * grad_scale;
@@ -249,10 +245,37 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
       mv[j] = mm;
       vv[j] = vvv;
     }
-    reinterpret_cast<f32x4*>(p)[i] = pv;
-    reinterpret_cast<f32x4*>(m)[i] = mv;
-    reinterpret_cast<f32x4*>(v)[i] = vv;
-    if (pb) reinterpret_cast<bf16x4*>(pb)[i] = bf16x4{f2bf(pv[0]), f2bf(pv[1]), f2bf(pv[2]), f2bf(pv[3])};
+  };
+  // 8 parameters per thread and iteration: the bf16 shadow leaves in one 16-B store (the 8-B form doubles the
+  // store instructions of that array), and twice the loads are in flight per wave
+  const size_t n8 = n4 / 2;
+  for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < n8; i += (size_t)gridDim.x * 256) {
+    f32x4 pv0 = reinterpret_cast<f32x4*>(p)[2 * i], pv1 = reinterpret_cast<f32x4*>(p)[2 * i + 1];
+    const f32x4 gv0 = reinterpret_cast<const f32x4*>(g)[2 * i], gv1 = reinterpret_cast<const f32x4*>(g)[2 * i + 1];
+    f32x4 mv0 = reinterpret_cast<f32x4*>(m)[2 * i], mv1 = reinterpret_cast<f32x4*>(m)[2 * i + 1];
+    f32x4 vv0 = reinterpret_cast<f32x4*>(v)[2 * i], vv1 = reinterpret_cast<f32x4*>(v)[2 * i + 1];
+    upd(pv0, gv0, mv0, vv0);
+    upd(pv1, gv1, mv1, vv1);
+    reinterpret_cast<f32x4*>(p)[2 * i] = pv0;
+    reinterpret_cast<f32x4*>(p)[2 * i + 1] = pv1;
+    reinterpret_cast<f32x4*>(m)[2 * i] = mv0;
+    reinterpret_cast<f32x4*>(m)[2 * i + 1] = mv1;
+    reinterpret_cast<f32x4*>(v)[2 * i] = vv0;
+    reinterpret_cast<f32x4*>(v)[2 * i + 1] = vv1;
+    if (pb)
+      reinterpret_cast<bf16x8*>(pb)[i] = bf16x8{f2bf(pv0[0]), f2bf(pv0[1]), f2bf(pv0[2]), f2bf(pv0[3]),
+                                                f2bf(pv1[0]), f2bf(pv1[1]), f2bf(pv1[2]), f2bf(pv1[3])};
+  }
+  if (n4 & 1) {  // an odd count of 4-parameter groups: the last one
+    const size_t i = n4 - 1;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      f32x4 pv = reinterpret_cast<f32x4*>(p)[i], mv = reinterpret_cast<f32x4*>(m)[i], vv = reinterpret_cast<f32x4*>(v)[i];
+      upd(pv, reinterpret_cast<const f32x4*>(g)[i], mv, vv);
+      reinterpret_cast<f32x4*>(p)[i] = pv;
+      reinterpret_cast<f32x4*>(m)[i] = mv;
+      reinterpret_cast<f32x4*>(v)[i] = vv;
+      if (pb) reinterpret_cast<bf16x4*>(pb)[i] = bf16x4{f2bf(pv[0]), f2bf(pv[1]), f2bf(pv[2]), f2bf(pv[3])};
+    }
   }
   sq = wave_sum(sq);
   __shared__ float r[4];

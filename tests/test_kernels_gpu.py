@@ -380,8 +380,8 @@ def test_xent(M, V, ld):
     assert torch.all(dl[:, V:] == 0)
 
 
-def test_adamw_matches_oracle_and_norm():
-    n = 4096 * 3
+@pytest.mark.parametrize("n", [4096 * 3, 4096 * 3 + 4])  # +4: an odd count of 4-parameter groups (the tail)
+def test_adamw_matches_oracle_and_norm(n):
     g = torch.Generator().manual_seed(11)
     p0, gr = torch.randn(n, generator=g), torch.randn(n, generator=g) * 0.01
     params = {"p": p0.clone()}

@@ -55,6 +55,8 @@ def main():
         return gemm_mode(libs, g, st)
     if os.environ.get("LIB_AB_OP") == "attn":
         return attn_mode(libs, g, st)
+    if os.environ.get("LIB_AB_OP") == "adamw":
+        return adamw_mode(libs, g, st)
     outs = {}
     for i, lib in enumerate(libs):
         for name, (m, n, A, B, sp, ws) in data.items():
@@ -206,6 +208,44 @@ def attn_mode(libs, g, st):
         for i in range(len(libs)):
             line += f"  lib{i}: {sorted(times[(i, n)])[2] * 1e3:8.1f} us"
         print(line, flush=True)
+
+
+
+def adamw_mode(libs, g, st):
+    """LIB_AB_OP=adamw: the fused AdamW over the 124M arena (with the bf16 shadow and the grad-norm partials);
+    parameters / moments / shadow compared bitwise against the first library after one step."""
+    n = 124_475_904
+    p0 = torch.randn(n, device=dev, generator=g)
+    gr = torch.randn(n, device=dev, generator=g) * 1e-3
+    res = []
+    for lib in libs:
+        p, m, v = p0.clone(), torch.zeros(n, device=dev), torch.zeros(n, device=dev)
+        pb = torch.empty(n, dtype=torch.bfloat16, device=dev)
+        part = torch.empty(4096, device=dev)
+        gn = torch.empty(1, device=dev)
+        res.append((p, m, v, pb, part, gn))
+    step = lambda lib, r: lib.gpt2mi_adamw(r[0].data_ptr(), gr.data_ptr(), r[1].data_ptr(), r[2].data_ptr(),  # noqa
+                                           r[3].data_ptr(), n, 1e-4, 0.1, 0.9, 0.95, 1e-8, 1, 1.0, r[4].data_ptr(),
+                                           r[5].data_ptr(), st)
+    for lib, r in zip(libs, res):
+        assert step(lib, r) == 0
+    torch.cuda.synchronize()
+    for i in range(1, len(libs)):
+        for k, name in enumerate(("p", "m", "v", "shadow")):
+            if not torch.equal(res[0][k], res[i][k]):
+                print(f"MISMATCH lib{i} {name}")
+        print(f"grad norm lib0 {res[0][5].item():.7g} lib{i} {res[i][5].item():.7g}")
+    times = {i: [] for i in range(len(libs))}
+    for _ in range(5):
+        for i, (lib, r) in enumerate(zip(libs, res)):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _r in range(5):
+                step(lib, r)
+            e.record()
+            torch.cuda.synchronize()
+            times[i].append(s.elapsed_time(e) / 5)
+    print("adamw " + "  ".join(f"lib{i}: {sorted(t)[2] * 1e3:8.1f} us" for i, t in times.items()), flush=True)
 
 
 if __name__ == "__main__":
