@@ -263,7 +263,7 @@ def _attn_ref(qkv, B, T, H):
     return q, k, v
 
 
-# B*H % 8 == 0 exercises the XCD-grouped block map, the others the plain one
+# B*H % 8 == 0: every head stays on one XCD under the heaviest-first block map; the others spread over XCDs
 @pytest.mark.parametrize("B,T,H", [(1, 64, 1), (2, 128, 2), (1, 1024, 2), (2, 256, 4), (4, 512, 6)])
 def test_attention_fwd_bwd(B, T, H):
     D = 64
