@@ -411,6 +411,29 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   if (P.alpha_dev) alpha *= P.alpha_dev[0];
   // [128][256] fp32 image (1 KiB rows) over the whole LDS; PERSIST: [64][256] in buffer 1
   float* img = reinterpret_cast<float*>(PERSIST ? buf1 : smem);
+  // accumulators of pass mi (tile rows mi*128 + rbase + 16i + (l & 15)) into image rows rbase + 16i + (l & 15); the
+  // alpha multiply only when alpha != 1 (one VALU per output element otherwise spent on every GEMM's epilogue)
+  auto write_image = [&](int mi, int rbase) {
+    auto body = [&](auto sc) {
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int r = rbase + 16 * i + (lane & 15);
+            const int c = BIL ? wc * 16 + ni * 8 + 4 * j + (lane >> 4) : ni * 32 + wc * 8 + 4 * j + (lane >> 4);
+            f32x4 v = acc[mi][ni][i][j];
+            if constexpr (decltype(sc)::value) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] *= alpha;
+            }
+            *reinterpret_cast<f32x4*>(img + r * 256 + 4 * (c ^ (r & 15))) = v;
+          }
+    };
+    if (alpha != 1.f) body(std::true_type{});
+    else body(std::false_type{});
+  };
   constexpr bool kOpnd = EPI == EPI_RESID || EPI == EPI_GELU_BWD || EPI == EPI_F32;
   // fused bias grad of the stored output (column sums of the rounded stores; reduced per tile below; the
   // persistent schedule has the registers for it only beside the GELU_BWD epilogue, the one that uses it)
@@ -442,19 +465,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
       }
       if (q) lds_barrier();  // the previous pass's reads are done before this pass overwrites the image
       if (wr == g) {
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-              const int r = 16 * i + (lane & 15);
-              const int c = ni * 32 + wc * 8 + 4 * j + (lane >> 4);
-              f32x4 v = acc[mi][ni][i][j];
-#pragma unroll
-              for (int e = 0; e < 4; ++e) v[e] *= alpha;
-              *reinterpret_cast<f32x4*>(img + r * 256 + 4 * (c ^ (r & 15))) = v;
-            }
+write_image(mi, 0);
       }
       lds_barrier();
       f32x4 va[4], vb[4];
@@ -512,19 +523,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
       }
       if (q) lds_barrier();  // the previous pass's reads are done before this pass overwrites the image
       if (wr == g) {
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-              const int r = 16 * i + (lane & 15);
-              const int c = ni * 32 + wc * 8 + 4 * j + (lane >> 4);
-              f32x4 v = acc[mi][ni][i][j];
-#pragma unroll
-              for (int e = 0; e < 4; ++e) v[e] *= alpha;
-              *reinterpret_cast<f32x4*>(img + r * 256 + 4 * (c ^ (r & 15))) = v;
-            }
+write_image(mi, 0);
       }
       lds_barrier();
       f32x4 v[8];
@@ -573,19 +572,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
               (size_t)min(m0 + mi * 128 + 16 * it + 2 * wid + hl, P.M - 1) * P.ldaux + gnb);
       }
       if (mi) lds_barrier();  // pass 0's reads are done before pass 1 overwrites the image
-#pragma unroll
-      for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const int r = wr * 64 + 16 * i + (lane & 15);
-            const int c = BIL ? wc * 16 + ni * 8 + 4 * j + (lane >> 4) : ni * 32 + wc * 8 + 4 * j + (lane >> 4);
-            f32x4 v = acc[mi][ni][i][j];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] *= alpha;
-            *reinterpret_cast<f32x4*>(img + r * 256 + 4 * (c ^ (r & 15))) = v;
-          }
+write_image(mi, wr * 64);
       lds_barrier();
       // VC: the per-tile switch (dropout for GELU, the fused column sums for BF16 / GELU_BWD); GUARD: partial
       // tile. Two halves of 4 row pairs (their 16 image reads in flight together; 32 VGPRs live, not 64)
@@ -650,19 +637,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
       }
     }
     if (mi) lds_barrier();  // pass 0's reads are done before pass 1 overwrites the image
-#pragma unroll
-    for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int r = wr * 64 + 16 * i + (lane & 15);
-          const int c = BIL ? wc * 16 + ni * 8 + 4 * j + (lane >> 4) : ni * 32 + wc * 8 + 4 * j + (lane >> 4);
-          f32x4 v = acc[mi][ni][i][j];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] *= alpha;
-          *reinterpret_cast<f32x4*>(img + r * 256 + 4 * (c ^ (r & 15))) = v;
-        }
+write_image(mi, wr * 64);
     lds_barrier();
     auto row_of = [&](int it) {
       const int r = it * 8 + wid;
