@@ -128,7 +128,7 @@ def main():
     torch.cuda.synchronize()
     if wrapped:
         dist.barrier()
-    probes = ["lm_head_fwd", "lm_head_dgrad", "lm_head_wgrad", "fc1_fwd", "attn_fwd"]
+    probes = ["lm_head_fwd", "lm_head_dgrad", "lm_head_wgrad", "fc1_fwd", "attn_fwd", "wgrad"]
     eng.probes = {p: [] for p in probes}
     torch.cuda.synchronize()
     if wrapped:
@@ -152,6 +152,9 @@ def main():
     kflops = {
         "lm_head_fwd": 2.0 * M * V * C, "lm_head_dgrad": 2.0 * M * V * C, "lm_head_wgrad": 2.0 * M * V * C,
         "fc1_fwd": 2.0 * M * 4 * C * C, "attn_fwd": 4.0 * B * H * (T * (T + 1) / 2) * (C // H),
+        # the weight-gradient family (one kernel, 1 + 4L launches a step: tied lm_head + qkv / proj / fc1 / fc2 of
+        # every block, each with its split-K reduction): the average algorithmic FLOPs of a launch
+        "wgrad": (2.0 * M * V * C + cfg.n_layer * 2.0 * M * 12 * C * C) / (1 + 4 * cfg.n_layer),
     }
     kernels = {}
     for name, evs in armed.items():

@@ -528,6 +528,10 @@ class Engine:
     # below is linear in it, so no GEMM here needs a scale. --
     def _wgrad(self, S, act, m, n, M, a, lda, b, ldb, out):
         # dW[m][n] += dY[:, :m]^T X[:, :n] over the M tokens
+        with self._probe("wgrad"):
+            self._wgrad_launch(S, act, m, n, M, a, lda, b, ldb, out)
+
+    def _wgrad_launch(self, S, act, m, n, M, a, lda, b, ldb, out):
         if act == F32:
             K.gemm(K.WGRAD, K.EPI_F32, m, n, M, a, lda, b, ldb, out, n, accumulate=True)
         elif m % 256 == 0 and n % 256 == 0:
@@ -679,7 +683,7 @@ class Engine:
             self._dgrad(act, M, ws.dln, ws.dlogits, "transformer.wte.weight", C, Vp, K.EPI_BF16, alpha_dev=alpha_dev,
                         alpha=gs)
         wte_g = self.layout.padded_view(self.grad, "transformer.wte.weight", Vp)
-        with self._probe("lm_head_wgrad"):
+        with self._probe("lm_head_wgrad"), self._probe("wgrad"):
             if C % 256 == 0 and act == BF16:
                 K.gemm_wgrad(Vp, C, M, ws.dlogits, Vp, ws.lnf, C, wte_g, C, accumulate=True, alpha_dev=alpha_dev,
                              alpha=gs, workspace=ws.wgrad_ws, splits=K_wgrad_splits(Vp, C, M))

@@ -1,7 +1,7 @@
 """Launch ONE of bench.py's probed kernels a few times on step-shaped inputs (GPT-2 124M, B=64, T=1024,
 dropout 0.1), for the rocprofv3 --pmc traffic passes (tools/pmc_traffic.sh -> profiles/traffic.json).
 
-    python tools/kernel_one.py <lm_head_fwd|lm_head_dgrad|lm_head_wgrad|fc1_fwd|attn_fwd|attn_bwd> [reps]
+    python tools/kernel_one.py <lm_head_fwd|lm_head_dgrad|lm_head_wgrad|fc1_fwd|attn_fwd|attn_bwd|wgrad> [reps]
 """
 import os
 import sys
@@ -49,6 +49,16 @@ def make(name):
         dqkv = torch.empty(M, 3 * C, dtype=torch.bfloat16, device=dev)
         p = float(os.environ.get("ATTN_P", "0.1"))
         return lambda: K.attn_bwd(qkv, out, dout, lse, delta, dqkv, B, T, H, C // H, p, 5)
+    if name == "wgrad":  # one step's weight gradients: 12 x (qkv, proj, fc1, fc2) + the tied lm_head
+        shapes = 12 * [(3 * C, C), (C, C), (4 * C, C), (C, 4 * C)] + [(Vp, C)]
+        ops = {(m, n): (r(M, m), r(M, n), torch.zeros(m, n, device=dev)) for m, n in set(shapes)}
+        ws = torch.empty(max(K.wgrad_splits(m, n, M) * m * n for m, n in shapes), device=dev)
+
+        def run():
+            for m, n in shapes:
+                a, x, g = ops[(m, n)]
+                K.gemm_wgrad(m, n, M, a, m, x, n, g, n, workspace=ws, splits=K.wgrad_splits(m, n, M))
+        return run
     raise SystemExit(f"unknown kernel {name}")
 
 

@@ -19,9 +19,16 @@ ALGO = {  # algorithmic bytes per launch (operands read once, outputs written on
     "lm_head_wgrad": 2 * (65536 * 50432 + 65536 * 768) + 4 * 2 * 50432 * 768,
     "fc1_fwd": 2 * (65536 * 768 + 3072 * 768 + 2 * 65536 * 3072) + 4 * 3072,
     "attn_fwd": 2 * (65536 * 2304 + 65536 * 768) + 4 * 768 * 1024,
+    # the weight-gradient family, averaged over one step's 49 launches: dY and X read once (bf16), dW read and
+    # written once (fp32, accumulated)
+    "wgrad": (12 * sum(2 * 65536 * (m + n) + 8 * m * n for m, n in ((2304, 768), (768, 768), (3072, 768), (768, 3072)))
+              + 2 * 65536 * (50432 + 768) + 8 * 50432 * 768) // 49,
 }
 # kernels whose counters make up one probed launch (the wgrad probe = split-K GEMM + slab reduction)
-KERNEL_KEY = {"attn_fwd": ("attn_fwd",), "lm_head_wgrad": ("gemm_pp", "splitk_reduce")}
+KERNEL_KEY = {"attn_fwd": ("attn_fwd",), "lm_head_wgrad": ("gemm_pp", "splitk_reduce"),
+              "wgrad": ("gemm_pp", "splitk_reduce")}
+# launches of one repetition of a family probe (the per-launch figure averages the last repetition's launches)
+FAMILY = {"wgrad": 49}
 
 
 def short(name):
@@ -29,12 +36,15 @@ def short(name):
     return name.split("(")[0]
 
 
-def per_launch(path, counter, keys):
+def per_launch(path, counter, keys, family=0):
     total, names = 0.0, []
     for key in keys:
         vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
                 if r["Counter_Name"] == counter and key in r["Kernel_Name"]]
-        vals = vals[1:] if len(vals) > 1 else vals  # drop the cold first launch
+        if family:  # a family probe: the mean over its last repetition's launches
+            vals = vals[-family:]
+        else:
+            vals = vals[1:] if len(vals) > 1 else vals  # drop the cold first launch
         total += sum(vals) / len(vals)
         names += sorted({short(r["Kernel_Name"]) for r in csv.DictReader(open(path)) if key in r["Kernel_Name"]})
     return total, " + ".join(names)
@@ -45,8 +55,10 @@ def main(root, probes):
     out = json.load(open(out_path)) if os.path.exists(out_path) else {}
     for p in probes:
         key = KERNEL_KEY.get(p, ("gemm_pp",))
-        fetch, kname = per_launch(os.path.join(root, f"{p}_fetch", "run_counter_collection.csv"), "FETCH_SIZE", key)
-        write, _ = per_launch(os.path.join(root, f"{p}_write", "run_counter_collection.csv"), "WRITE_SIZE", key)
+        fam = FAMILY.get(p, 0)
+        fetch, kname = per_launch(os.path.join(root, f"{p}_fetch", "run_counter_collection.csv"), "FETCH_SIZE", key,
+                                  fam)
+        write, _ = per_launch(os.path.join(root, f"{p}_write", "run_counter_collection.csv"), "WRITE_SIZE", key, fam)
         hbm = (2 * fetch + write) * 1024
         out[p] = {"kernel": kname, "fetch_size_kb": round(fetch, 1), "write_size_kb": round(write, 1),
                   "hbm_bytes_per_launch": int(hbm), "algorithmic_bytes_per_launch": ALGO[p],
