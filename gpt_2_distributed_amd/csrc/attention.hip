@@ -30,7 +30,11 @@ namespace {
 constexpr int D = 64;
 constexpr int BQ = 128;  // queries per workgroup in fwd / dQ (32 per wave = two 16-query MFMA groups)
 constexpr int BKV = 64;  // keys per K/V tile in fwd / dQ
-constexpr int BKB = 128; // keys per workgroup in dK/dV (32 per wave)
+#ifndef ATTN_DKDV_WAVES
+#define ATTN_DKDV_WAVES 4
+#endif
+constexpr int kDkdvWaves = ATTN_DKDV_WAVES;  // waves per dK/dV workgroup (32 keys each)
+constexpr int BKB = 32 * kDkdvWaves;        // keys per workgroup in dK/dV
 constexpr int BQT = 64;  // queries per Q/dO tile in dK/dV
 constexpr int kThreads = 256;
 constexpr float kLog2e = 1.4426950408889634f;
@@ -143,11 +147,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t qkv_rsrc(const bf16* base) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
 }
 // rows [row0, row0 + 64) x cols [col0, col0 + 64) of the buffer (row stride ld elements)
+template <int NW = 4>  // waves of the workgroup sharing the tile's 8 instructions
 __device__ __forceinline__ void tile_dma(char* lds, __amdgpu_buffer_rsrc_t rs, int row0, int col0, int ld,
                                          uint32_t loff, int w) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int ins = 2 * w + i;
+  for (int i = 0; i < 8 / NW; ++i) {
+    const int ins = (8 / NW) * w + i;
     const int soff = ((row0 + 8 * ins) * ld + col0) * (int)sizeof(bf16);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(lds + ins * 1024), 16, loff, soff, 0, 0);
   }
@@ -471,7 +476,7 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const bf16* __
 // ---------------------------------------------------------------------------------------------
 // dK, dV: key-outer (128 keys per workgroup, 32 per wave) over 64-query tiles at or after the keys.
 template <bool DROP>
-__global__ __launch_bounds__(kThreads, 2) void attn_bwd_dkdv_kernel(const bf16* __restrict__ qkv,
+__global__ __launch_bounds__(64 * kDkdvWaves) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_bwd_dkdv_kernel(const bf16* __restrict__ qkv,
                                                                     const bf16* __restrict__ dout,
                                                                     const float* __restrict__ lse,
                                                                     const float* __restrict__ delta,
@@ -519,8 +524,8 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dkdv_kernel(const bf16* 
   const __amdgpu_buffer_rsrc_t rsq = qkv_rsrc(base), rsd = qkv_rsrc(dout + (size_t)b * T * C);
   // Q / dO tiles by LDS-DMA straight into stage `st`; lse / delta by registers (scaled at their LDS write)
   auto gload = [&](int i, char* st) {
-    tile_dma(st, rsq, i * BQT, h * D, (int)ld, qoff, wu);
-    tile_dma(st + kTile, rsd, i * BQT, h * D, C, doff, wu);
+    tile_dma<kDkdvWaves>(st, rsq, i * BQT, h * D, (int)ld, qoff, wu);
+    tile_dma<kDkdvWaves>(st + kTile, rsd, i * BQT, h * D, C, doff, wu);
     if (threadIdx.x < BQT) {  // raw values: any use here would wait (in-order vmcnt) for the tiles above too
       rl = lrow[i * BQT + threadIdx.x];
       rdl = drow[i * BQT + threadIdx.x];
@@ -687,10 +692,10 @@ GPT2MI_EXPORT int gpt2mi_attn_bwd(const uint16_t* qkv, const uint16_t* out, cons
   if (rc) return rc;
   const dim3 gkv((T + BKB - 1) / BKB, B * H);
   if (thr)
-    attn_bwd_dkdv_kernel<true><<<gkv, kThreads, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta,
+    attn_bwd_dkdv_kernel<true><<<gkv, 64 * kDkdvWaves, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta,
                                                         (bf16*)dqkv, dqkv_colsum, T, H, scale, seed, thr, ik);
   else
-    attn_bwd_dkdv_kernel<false><<<gkv, kThreads, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta,
+    attn_bwd_dkdv_kernel<false><<<gkv, 64 * kDkdvWaves, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta,
                                                          (bf16*)dqkv, dqkv_colsum, T, H, scale, seed, thr, ik);
   return gpt2mi::check_launch("attn_bwd_dkdv");
 }
