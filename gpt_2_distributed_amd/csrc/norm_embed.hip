@@ -379,7 +379,12 @@ static int layernorm_bwd_t(const float* x, const float* w, const float* mean, co
   GPT2MI_REQUIRE(p_out <= 0.f || (size_t)M * C < (1ull << 33),
                  "layernorm_bwd: M*C exceeds the 32-bit dropout pair index");
   hipStream_t s = (hipStream_t)stream;
-  const int g = grid_rows(M) > 2048 ? 2048 : grid_rows(M);
+#ifndef LN_BWD_MAX_BLOCKS
+#define LN_BWD_MAX_BLOCKS 512
+#endif
+  // the column-sum flush is one atomic per column per block: fewer blocks, fewer atomics (tools/ln_probe.py at cfg 2:
+  // 2048 blocks 157-158 us, 1024 158, 512 153 — 8 waves per CU still stream at the HBM limit)
+  const int g = grid_rows(M) > LN_BWD_MAX_BLOCKS ? LN_BWD_MAX_BLOCKS : grid_rows(M);
   const size_t sh = (size_t)kWaves * C * sizeof(float);
   const uint32_t thr = drop_threshold(p_out);
   const float ik = p_out > 0.f ? 1.f / (1.f - p_out) : 1.f;
