@@ -57,6 +57,8 @@ def main():
         return attn_mode(libs, g, st)
     if os.environ.get("LIB_AB_OP") == "adamw":
         return adamw_mode(libs, g, st)
+    if os.environ.get("LIB_AB_OP") == "xent":
+        return xent_mode(libs, g, st)
     outs = {}
     for i, lib in enumerate(libs):
         for name, (m, n, A, B, sp, ws) in data.items():
@@ -246,6 +248,42 @@ def adamw_mode(libs, g, st):
             torch.cuda.synchronize()
             times[i].append(s.elapsed_time(e) / 5)
     print("adamw " + "  ".join(f"lib{i}: {sorted(t)[2] * 1e3:8.1f} us" for i, t in times.items()), flush=True)
+
+
+def xent_mode(libs, g, st):
+    """LIB_AB_OP=xent: the register-resident cross-entropy (loss rows, lse, bf16 dlogits) at cfg 2's head
+    (65536 rows of 50257 logits, row stride 50304); outputs compared bitwise against the first library."""
+    M, V, ld = 65536, 50257, 50304
+    logits = (torch.randn(M, ld, device=dev, generator=g) * 2).to(torch.bfloat16)
+    labels = torch.randint(0, V, (M,), device=dev, generator=g)
+    labels[::97] = -100
+    res = []
+    for lib in libs:
+        res.append((torch.empty(M, device=dev), torch.empty(M, device=dev), torch.empty_like(logits),
+                    torch.empty(1, device=dev), torch.empty(1, device=dev)))
+    run = lambda lib, r: lib.gpt2mi_xent_fwd(logits.data_ptr(), ld, labels.data_ptr(), r[0].data_ptr(),  # noqa
+                                             r[1].data_ptr(), r[2].data_ptr(), ld, M, V, -100, r[3].data_ptr(),
+                                             r[4].data_ptr(), st)
+    for lib, r in zip(libs, res):
+        assert run(lib, r) == 0
+    torch.cuda.synchronize()
+    for i in range(1, len(libs)):
+        for k, name in enumerate(("loss_rows", "lse", "dlogits", "loss")):
+            if not torch.equal(res[0][k], res[i][k]):
+                print(f"MISMATCH lib{i} {name}")
+    times = {i: [] for i in range(len(libs))}
+    for _ in range(5):
+        for i, (lib, r) in enumerate(zip(libs, res)):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _r in range(5):
+                run(lib, r)
+            e.record()
+            torch.cuda.synchronize()
+            times[i].append(s.elapsed_time(e) / 5)
+    gb = 2 * 2 * M * ld / 1e9
+    print("xent " + "  ".join(f"lib{i}: {sorted(t)[2] * 1e3:8.1f} us {gb / sorted(t)[2]:5.2f} TB/s"
+                              for i, t in times.items()), flush=True)
 
 
 if __name__ == "__main__":
