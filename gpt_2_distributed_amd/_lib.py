@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("GPT2MI_LIB") or os.path.join(_HERE, "libgpt2mi.so")
 
 # the ABI these bindings are written against (include/gpt2mi.h GPT2MI_ABI_VERSION): a stale or foreign
 # library is refused at load instead of being called with the wrong argument lists
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 _c_int, _c_float, _c_size, _c_u64, _p = ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_void_p
 
@@ -45,6 +45,7 @@ _SIGS = {
     "gpt2mi_transpose_bf16_batched": [_p, _p, _p, _c_int, ctypes.c_int64, _p],
     "gpt2mi_scale_mul": [_p, _p, _p, _p],
     "gpt2mi_memset_zero": [_p, _c_size, _p],
+    "gpt2mi_zero_ranges": [_p, _p, _c_int, _p],
     "gpt2mi_set_gemm_impl": [_c_int],
     "gpt2mi_set_gemm_persistent": [_c_int],
     "gpt2mi_gemm_f32": [_c_int, _c_int, _c_int, _c_int, _c_int, _p, _c_int, _p, _c_int, _p, _c_int, _p, _p, _p,
@@ -278,6 +279,12 @@ def scale_mul(a, b, out):
 
 def zero_(t: torch.Tensor):
     _call("gpt2mi_memset_zero", _ptr(t), t.numel() * t.element_size(), _stream())
+
+
+def zero_ranges(t: torch.Tensor, ranges: torch.Tensor):
+    """Zero the element ranges of fp32 t given as a cuda int64 [n, 2] tensor of (offset, count)."""
+    assert t.dtype == torch.float32 and ranges.dtype == torch.int64 and ranges.is_cuda
+    _call("gpt2mi_zero_ranges", _ptr(t), _ptr(ranges), ranges.shape[0], _stream())
 
 
 def set_gemm_impl(impl: int):

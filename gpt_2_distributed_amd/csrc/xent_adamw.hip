@@ -414,6 +414,20 @@ GPT2MI_EXPORT int gpt2mi_scale_mul(const float* a, const float* b, float* out, v
   return gpt2mi::check_launch("scale_mul");
 }
 
+// Zero n ranges [off, off+cnt) of a float array in one launch (blockIdx.y = range; ranges = device int64 pairs):
+// the grad arena's atomically accumulated slots before a backward whose GEMMs write the weight slots outright.
+__global__ __launch_bounds__(256) void zero_ranges_kernel(float* __restrict__ base, const int64_t* __restrict__ ranges) {
+  const int64_t off = ranges[2 * blockIdx.y], cnt = ranges[2 * blockIdx.y + 1];
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < cnt; i += (int64_t)gridDim.x * 256) base[off + i] = 0.f;
+}
+
+GPT2MI_EXPORT int gpt2mi_zero_ranges(float* base, const int64_t* ranges, int n, void* stream) {
+  GPT2MI_REQUIRE(n >= 0 && n <= 65535, "zero_ranges: %d ranges (at most 65535)", n);
+  if (n == 0) return 0;
+  zero_ranges_kernel<<<dim3(64, n), 256, 0, (hipStream_t)stream>>>(base, ranges);
+  return gpt2mi::check_launch("zero_ranges");
+}
+
 GPT2MI_EXPORT int gpt2mi_memset_zero(void* ptr, size_t bytes, void* stream) {
   hipError_t e = hipMemsetAsync(ptr, 0, bytes, (hipStream_t)stream);
   if (e != hipSuccess) {

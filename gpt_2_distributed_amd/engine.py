@@ -271,6 +271,10 @@ class Engine:
         self.grad_sync: Optional[GradHooks] = None  # set by data-parallel wrappers (parallel.py)
         self.param_provider = None  # FSDP: owns the full parameter views (gathers them per unit)
         self.grad_dirty = False     # the grad arena holds gradients of an earlier backward (accumulation)
+        # the weight-gradient GEMMs of the running backward write their slots outright: set by a full backward
+        # that starts from zero_grad(set_to_none=True), which then zeroes only the accumulated slots
+        self._grad_fresh = False
+        self._acc_ranges = None     # cuda int64 [n, 2]: the arena ranges outside the GEMM-written weight slots
         self.bwd_act = F32
         self._params = list(model.parameters())
         self.params_by_name = dict(model.named_parameters())
@@ -368,11 +372,41 @@ class Engine:
         K.zero_(self.grad)
         self.grad_dirty = False
 
-    def _prepare_grads(self):
+    def _lazy_zero_ok(self, act):
+        # every weight-gradient GEMM of the full backward takes a path with a write-or-accumulate choice
+        # (gemm_wgrad / EPI_F32; not the EPI_ATOMIC fallback of widths that are not multiples of 256), and
+        # the arena is the engine's own (FSDP zeroes per unit)
+        return act == BF16 and self.param_provider is None and self.cfg.n_embd % 256 == 0
+
+    def _zero_accumulated(self):
+        """Zero the arena outside the GEMM-written weight slots (wte with its pad rows, the four matrices of
+        every block): LayerNorm params, biases, wpe, ln_f and the alignment gaps, in one launch."""
+        if self._acc_ranges is None:
+            gemm = sorted((sl.offset, sl.offset + sl.reserved) for n, sl in self.layout.slots.items()
+                          if n in self._t_weights)
+            rng, pos = [], 0
+            for a, b in gemm:
+                if a > pos:
+                    rng.append((pos, a - pos))
+                pos = max(pos, b)
+            if pos < self.grad.numel():
+                rng.append((pos, self.grad.numel() - pos))
+            self._acc_ranges = torch.tensor(rng, dtype=torch.int64).to(self.device)
+        K.zero_ranges(self.grad, self._acc_ranges)
+
+    def _prepare_grads(self, full_backward_act=None):
         """Accumulate into the arena when p.grad are its views; start from zero after a
-        zero_grad(set_to_none=True) (every p.grad None)."""
+        zero_grad(set_to_none=True) (every p.grad None). full_backward_act: the precision of a backward that
+        forms EVERY weight gradient (the whole-model loss backward): its GEMMs then write the weight slots
+        and only the rest of the arena is zeroed."""
+        self._grad_fresh = False
         if all(p.grad is None for p in self.params_by_name.values()):
-            self.zero_grad()
+            if full_backward_act is not None and self._lazy_zero_ok(full_backward_act):
+                self._zero_accumulated()
+                self._grad_fresh = True
+                self.grad_dirty = False
+            else:
+                self.zero_grad()
             self.bind_grads()
             return
         for n, p in self.params_by_name.items():
@@ -380,10 +414,10 @@ class Engine:
                 raise RuntimeError(f"{n}.grad is not a view of the engine's grad arena; zero grads with "
                                    "set_to_none=True or the model's optimizer before backward")
 
-    def _begin_grads(self, act) -> float:
+    def _begin_grads(self, act, full=False) -> float:
         if act == BF16 and self.param_provider is None and self._shadowT_stale:
             self.refresh_shadowT()  # the dgrads read W^T (a forward run without grad did not build it)
-        self._prepare_grads()
+        self._prepare_grads(act if full else None)
         self.bwd_act = act  # the precision of this backward's gradients (FSDP reduces in it)
         scale = self.grad_sync.begin_backward() if self.grad_sync is not None else 1.0
         self.grad_dirty = True
@@ -394,6 +428,7 @@ class Engine:
             self.grad_sync.ready(name)
 
     def _end_grads(self):
+        self._grad_fresh = False
         if self.grad_sync is not None:
             self.grad_sync.end_backward()
 
@@ -533,11 +568,12 @@ class Engine:
 
     def _wgrad_launch(self, S, act, m, n, M, a, lda, b, ldb, out):
         if act == F32:
-            K.gemm(K.WGRAD, K.EPI_F32, m, n, M, a, lda, b, ldb, out, n, accumulate=True)
+            K.gemm(K.WGRAD, K.EPI_F32, m, n, M, a, lda, b, ldb, out, n, accumulate=not self._grad_fresh)
         elif m % 256 == 0 and n % 256 == 0:
-            K.gemm_wgrad(m, n, M, a, lda, b, ldb, out, n, accumulate=True, workspace=S.wgrad_ws,
+            K.gemm_wgrad(m, n, M, a, lda, b, ldb, out, n, accumulate=not self._grad_fresh, workspace=S.wgrad_ws,
                          splits=K_wgrad_splits(m, n, M))
         else:
+            assert not self._grad_fresh, "atomic weight gradients need a zeroed arena"
             s = self.WGRAD_SPLITS
             while s > 1 and M % (64 * s) != 0:
                 s //= 2
@@ -669,7 +705,7 @@ class Engine:
         if not use_loss and grad_logits is None:
             self._prepare_grads()
             return
-        gs = self._begin_grads(act)
+        gs = self._begin_grads(act, full=True)
         alpha_dev = None
         if use_loss:  # d(loss)/d(logit) = grad_loss / #valid labels times the unscaled dlogits
             K.scale_mul(grad_loss.reshape(1).to(F32), ws.inv_count, ws.dscale)
@@ -685,11 +721,11 @@ class Engine:
         wte_g = self.layout.padded_view(self.grad, "transformer.wte.weight", Vp)
         with self._probe("lm_head_wgrad"), self._probe("wgrad"):
             if C % 256 == 0 and act == BF16:
-                K.gemm_wgrad(Vp, C, M, ws.dlogits, Vp, ws.lnf, C, wte_g, C, accumulate=True, alpha_dev=alpha_dev,
-                             alpha=gs, workspace=ws.wgrad_ws, splits=K_wgrad_splits(Vp, C, M))
+                K.gemm_wgrad(Vp, C, M, ws.dlogits, Vp, ws.lnf, C, wte_g, C, accumulate=not self._grad_fresh,
+                             alpha_dev=alpha_dev, alpha=gs, workspace=ws.wgrad_ws, splits=K_wgrad_splits(Vp, C, M))
             else:
                 K.gemm(K.WGRAD, K.EPI_F32, Vp, C, M, ws.dlogits, Vp, ws.lnf, C, wte_g, C, alpha_dev=alpha_dev,
-                       alpha=gs, accumulate=True)
+                       alpha=gs, accumulate=not self._grad_fresh)
         self._trunk_bwd(ws, sv)
         self._end_grads()
 

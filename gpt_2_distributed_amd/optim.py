@@ -67,14 +67,22 @@ class FusedAdamW(_FlatAdamW):
             with torch.enable_grad():
                 loss = closure()
         eng = self.engine
+        if all(p.grad is None for p in eng.params_by_name.values()):
+            return loss  # no gradients since zero_grad(set_to_none=True): torch's optimizers skip such params
         self._run(self.model.arena, eng.grad, eng.shadow)
         eng.mark_shadow_fresh()
         return loss
 
     def zero_grad(self, set_to_none: bool = True):
-        # The grads are views of one arena: zero it in one memset and keep the views bound.
-        self.engine.zero_grad()
-        self.engine.bind_grads()
+        # The grads are views of one arena. set_to_none (torch's default): unbind them; the next backward
+        # rebinds, and a whole-model backward then zeroes only the accumulated slots (its weight-gradient
+        # GEMMs write theirs). Otherwise zero the arena in one memset and keep the views bound.
+        if set_to_none:
+            for p in self.engine.params_by_name.values():
+                p.grad = None
+        else:
+            self.engine.zero_grad()
+            self.engine.bind_grads()
 
 
 class ShardedAdamW(_FlatAdamW):

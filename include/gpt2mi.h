@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GPT2MI_ABI_VERSION 6
+#define GPT2MI_ABI_VERSION 7
 
 const char* gpt2mi_last_error(void);
 int gpt2mi_abi_version(void); /* returns GPT2MI_ABI_VERSION of the built library */
@@ -179,6 +179,11 @@ int gpt2mi_fsdp_pack(const float* src, void* dst, int dst_f32, size_t n, size_t 
 int gpt2mi_fsdp_accum(const void* src, int src_f32, float* dst, size_t n, int accumulate, void* stream);
 int gpt2mi_scale_mul(const float* a, const float* b, float* out, void* stream);
 int gpt2mi_memset_zero(void* ptr, size_t bytes, void* stream);
+/* Zero n element ranges of a float array in one launch; ranges = DEVICE int64 pairs (offset, count).
+ * Replaces, for the atomically accumulated slots of the grad arena (LayerNorm params, biases, wpe, ln_f),
+ * the full-arena zero of optimizer.zero_grad() (torch/optim/optimizer.py zero_grad via
+ * train_gpt2_distributed.py:409-425) when the backward's weight-gradient GEMMs write their slots outright. */
+int gpt2mi_zero_ranges(float* base, const int64_t* ranges, int n, void* stream);
 
 #ifdef __cplusplus
 }

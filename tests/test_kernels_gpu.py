@@ -380,6 +380,17 @@ def test_xent(M, V, ld):
     assert torch.all(dl[:, V:] == 0)
 
 
+def test_zero_ranges():
+    t = torch.randn(300_000, device=dev)
+    ref = t.clone()
+    rng = [(0, 1), (5, 1000), (2000, 0), (70_000, 200_001), (299_999, 1)]
+    for o, c in rng:
+        ref[o:o + c] = 0
+    L().zero_ranges(t, torch.tensor(rng, dtype=torch.int64).to(dev))
+    torch.cuda.synchronize()
+    assert torch.equal(t, ref)
+
+
 @pytest.mark.parametrize("n", [4096 * 3, 4096 * 3 + 4])  # +4: an odd count of 4-parameter groups (the tail)
 def test_adamw_matches_oracle_and_norm(n):
     g = torch.Generator().manual_seed(11)

@@ -370,3 +370,49 @@ def test_b64_step_equals_the_mean_of_b4_chunks():
         b = small[sl.offset:sl.offset + sl.numel]
         e = float((a - b).double().norm() / (b.double().norm() + 1e-30))
         assert e < 1e-3, (n, e)
+
+
+def test_lazy_zero_grad_matches_memset():
+    """zero_grad(set_to_none=True) before a whole-model backward zeroes only the accumulated slots; the weight-
+    gradient GEMMs write theirs. Against a backward into a memset arena: block weight slots bitwise equal (0 + s =
+    s), the atomically summed slots (wte takes the embedding backward's atomics too) equal to atomic-order rounding, and nothing stale survives (the lazily zeroed
+    arena starts full of garbage)."""
+    from gpt_2_distributed_amd.model import GPT2, GPT2Config
+    cfg = GPT2Config(n_layer=2, n_head=4, n_embd=256, vocab_size=509, n_positions=64, resid_pdrop=0.1, attn_pdrop=0.1)
+    a, b = GPT2(cfg).to(dev), GPT2(cfg).to(dev)
+    oa, ob = a.configure_optimizers(learning_rate=1e-3), b.configure_optimizers(learning_rate=1e-3)
+    g = torch.Generator().manual_seed(5)
+    x = torch.randint(0, 509, (4, 64), generator=g).to(dev)
+    y = torch.randint(0, 509, (4, 64), generator=g).to(dev)
+    oa.zero_grad(set_to_none=True)
+    assert all(p.grad is None for p in a.parameters())
+    a.engine().grad.fill_(123.0)
+    ob.zero_grad(set_to_none=False)
+    for m in (a, b):
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            _, loss = m(x, labels=y)
+        loss.backward()
+    ga, gb = a.engine().grad, b.engine().grad
+    torch.cuda.synchronize()
+    assert not a.engine()._grad_fresh
+    gemm = set(a.engine()._t_weights)
+    assert "transformer.wte.weight" in gemm and len(gemm) == 1 + 4 * cfg.n_layer
+    covered = torch.zeros(ga.numel(), dtype=torch.bool)
+    for n, sl in a.layout.slots.items():
+        covered[sl.offset:sl.offset + sl.reserved] = True
+        sa, sb = ga[sl.offset:sl.offset + sl.reserved], gb[sl.offset:sl.offset + sl.reserved]
+        if n in gemm and "wte" not in n:  # wte: + the embedding backward's atomics (any order)
+            assert torch.equal(sa, sb), n
+        else:
+            assert torch.allclose(sa, sb, rtol=1e-5, atol=1e-7), n
+    assert torch.all(ga[~covered.to(dev)] == 0)  # the alignment gaps
+    # a step right after zero_grad(set_to_none=True) has no gradients to apply: torch's optimizers skip it
+    before = a.arena.clone()
+    oa.step()
+    oa.zero_grad(set_to_none=True)
+    oa.step()
+    torch.cuda.synchronize()
+    assert not torch.equal(before, a.arena)
+    after = a.arena.clone()
+    oa.step()
+    assert torch.equal(after, a.arena)
