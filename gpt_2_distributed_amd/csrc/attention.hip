@@ -411,7 +411,10 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const bf16* __
       f32x4 s[2][4], dp[2][4];
 #pragma unroll
       for (int fi = 0; fi < 4; ++fi) {
-        s[0][fi] = s[1][fi] = dp[0][fi] = dp[1][fi] = f32x4{0.f, 0.f, 0.f, 0.f};
+        // dP' accumulates onto -delta (the query's row constant), so a kept entry's dP' - delta leaves the chain
+        s[0][fi] = s[1][fi] = f32x4{0.f, 0.f, 0.f, 0.f};
+        dp[0][fi] = f32x4{-dl[0], -dl[0], -dl[0], -dl[0]};
+        dp[1][fi] = f32x4{-dl[1], -dl[1], -dl[1], -dl[1]};
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
           const bf16x8 kf = row_frag(Ks, 16 * fi, kk, lane);
@@ -439,9 +442,9 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const bf16* __
             for (int qg = 0; qg < 2; ++qg) {
               float p = __builtin_amdgcn_exp2f(fmaf(s[qg][fi][r], sl2, -lse2[qg]));
               if constexpr (DIAG) p = (k_lo + 16 * fi + 4 * g + r > q_lo + 16 * qg + (lane & 15)) ? 0.f : p;
-              float d = dp[qg][fi][r];
-              if constexpr (DROP) d = drop_keep16(hh, qg, thr) ? d : 0.f;
-              s[qg][fi][r] = p * (d - dl[qg]);
+              float d = dp[qg][fi][r];  // dP' - delta
+              if constexpr (DROP) d = drop_keep16(hh, qg, thr) ? d : -dl[qg];
+              s[qg][fi][r] = p * d;
             }
           }
       };
@@ -557,10 +560,18 @@ __global__ __launch_bounds__(64 * kDkdvWaves) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
       for (int hq = 0; hq < 2; ++hq) {
         f32x4 s[2][2], dp[2][2];  // [kg][fl]: S[q = q0 + 16(2hq+fl) + 4g + r][key = k_lo + 16kg + (l&15)]
+        f32x4 l4[2], d4[2];
+#pragma unroll
+        for (int fl = 0; fl < 2; ++fl) {
+          l4[fl] = *reinterpret_cast<const f32x4*>(Ls + 16 * (2 * hq + fl) + 4 * g);
+          d4[fl] = *reinterpret_cast<const f32x4*>(Dl + 16 * (2 * hq + fl) + 4 * g);
+        }
 #pragma unroll
         for (int fl = 0; fl < 2; ++fl) {
           const int fi = 2 * hq + fl;
-          s[0][fl] = s[1][fl] = dp[0][fl] = dp[1][fl] = f32x4{0.f, 0.f, 0.f, 0.f};
+          // dP' accumulates onto -delta (the rows' constants), so a kept entry's dP' - delta leaves the chain
+          s[0][fl] = s[1][fl] = f32x4{0.f, 0.f, 0.f, 0.f};
+          dp[0][fl] = dp[1][fl] = -d4[fl];
 #pragma unroll
           for (int kk = 0; kk < 2; ++kk) {
             const bf16x8 qa = row_frag(Qs, 16 * fi, kk, lane);
@@ -571,12 +582,6 @@ __global__ __launch_bounds__(64 * kDkdvWaves) __attribute__((amdgpu_waves_per_eu
               dp[kg][fl] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, vf[kg][kk], dp[kg][fl], 0, 0, 0);
             }
           }
-        }
-        f32x4 l4[2], d4[2];
-#pragma unroll
-        for (int fl = 0; fl < 2; ++fl) {
-          l4[fl] = *reinterpret_cast<const f32x4*>(Ls + 16 * (2 * hq + fl) + 4 * g);
-          d4[fl] = *reinterpret_cast<const f32x4*>(Dl + 16 * (2 * hq + fl) + 4 * g);
         }
         // P = exp2(S*scale*log2e - LSE*log2e); dropped entries: P_drop = 0 (dV; its 1/(1-p) is applied
         // to dV at the end) and dP = 0 (dS); dP already carries 1/(1-p) through the prescaled V.
@@ -594,14 +599,14 @@ __global__ __launch_bounds__(64 * kDkdvWaves) __attribute__((amdgpu_waves_per_eu
               for (int fl = 0; fl < 2; ++fl) {
                 float p = __builtin_amdgcn_exp2f(fmaf(s[kg][fl][r], sl2, -l4[fl][r]));
                 if constexpr (DIAG) p = (q0 + 16 * (2 * hq + fl) + 4 * g + r < key) ? 0.f : p;
-                float pdv = p, d = dp[kg][fl][r];
+                float pdv = p, d = dp[kg][fl][r];  // dP' - delta
                 if constexpr (DROP) {
                   const bool keep = drop_keep16(hh, fl, thr);
                   pdv = keep ? p : 0.f;
-                  d = keep ? d : 0.f;
+                  d = keep ? d : -d4[fl][r];
                 }
-                dp[kg][fl][r] = pdv;                 // dropped P (for dV)
-                s[kg][fl][r] = p * (d - d4[fl][r]);  // dS
+                dp[kg][fl][r] = pdv;  // dropped P (for dV)
+                s[kg][fl][r] = p * d;  // dS
               }
             }
           }
