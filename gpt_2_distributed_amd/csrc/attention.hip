@@ -30,6 +30,9 @@ namespace {
 constexpr int D = 64;
 constexpr int BQ = 128;  // queries per workgroup in fwd / dQ (32 per wave = two 16-query MFMA groups)
 constexpr int BKV = 64;  // keys per K/V tile in fwd / dQ
+#ifndef ATTN_FWD_OCC
+#define ATTN_FWD_OCC 3  // forward waves per SIMD the register budget is cut for (launch bounds)
+#endif
 #ifndef ATTN_DKDV_WAVES
 #define ATTN_DKDV_WAVES 4
 #endif
@@ -178,7 +181,7 @@ __device__ __forceinline__ void attn_block(int& bh, int& blk) {
 
 // ---------------------------------------------------------------------------------------------
 template <bool DROP>
-__global__ __launch_bounds__(kThreads, 3) void attn_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
+__global__ __launch_bounds__(kThreads, ATTN_FWD_OCC) void attn_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
                                                                float* __restrict__ lse, int T, int H, float scale,
                                                                uint64_t seed, uint32_t thr, float inv_keep) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * BKV * 128];  // 2 stages x (K, V)
