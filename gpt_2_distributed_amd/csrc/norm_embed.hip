@@ -269,40 +269,39 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restric
   }
 }
 
-// Embedding backward, token table: dwte[idx[m],:] += dres[m,:]*keep/(1-p) (fp32 atomics; the
-// tied lm_head wgrad has already been written into the same rows).
-__global__ __launch_bounds__(256) void embed_bwd_wte_kernel(const int64_t* __restrict__ idx, const float* __restrict__ dres,
-                                                            float* __restrict__ dwte, int M, int T, int T_valid, int C,
-                                                            uint64_t seed, uint32_t thr, float inv_keep) {
-  const int lane = threadIdx.x & 63;
-  for (int row = blockIdx.x * kWaves + (threadIdx.x >> 6); row < M; row += gridDim.x * kWaves) {
-    if (row % T >= T_valid) continue;  // padding rows carry no gradient
-    const int64_t tok = idx[row];
-    float* dst = dwte + (size_t)tok * C;
-    const float* src = dres + (size_t)row * C;
-    for (int c = lane; c < C; c += 64) {
-      float g = src[c];
-      if (thr) g = drop_keep(seed, (uint64_t)row * C + c, thr) ? g * inv_keep : 0.f;
-      atomicAdd(dst + c, g);
-    }
-  }
-}
-
-// Embedding backward, position table: dwpe[t,c] += sum_b dres[b,t,c]*keep/(1-p). No atomics:
-// one thread per (t, c) column walks the batch.
-__global__ __launch_bounds__(256) void embed_bwd_wpe_kernel(const float* __restrict__ dres, float* __restrict__ dwpe,
-                                                            int B, int T, int T_valid, int C, uint64_t seed,
-                                                            uint32_t thr, float inv_keep) {
+// Embedding backward (model.py:295-304 reversed), both tables in one pass over the residual gradient, the dropout
+// mask hashed once per element: one thread per (t, c) walks the batch,
+//   g = dres[b,t,c]*keep/(1-p);  dwte[idx[b,t],c] += g (fp32 atomics, 256 contiguous bytes per wave instruction;
+//   the tied lm_head wgrad has already written those rows);  dwpe[t,c] += sum_b g (no atomics, batch order).
+// (Two kernels before: the token-table one and the position-table one each re-hashed every element: 169 + 66 us.)
+__global__ __launch_bounds__(256) void embed_bwd_kernel(const int64_t* __restrict__ idx, const float* __restrict__ dres,
+                                                        float* __restrict__ dwte, float* __restrict__ dwpe, int B,
+                                                        int T, int T_valid, int C, uint64_t seed, uint32_t thr,
+                                                        float inv_keep) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= T_valid * C) return;  // rows of wpe past T_valid are not touched (they may not exist)
   const int t = i / C, c = i % C;
   float s = 0.f;
-  for (int b = 0; b < B; ++b) {
+  auto one = [&](int b, float g, int64_t tok) {
     const size_t row = (size_t)b * T + t;
-    float g = dres[row * C + c];
     if (thr) g = drop_keep(seed, row * C + c, thr) ? g * inv_keep : 0.f;
     s += g;
+    atomicAdd(dwte + (size_t)tok * C + c, g);
+  };
+  int b = 0;
+  for (; b + 4 <= B; b += 4) {  // the four rows' loads first
+    float g[4];
+    int64_t tok[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const size_t row = (size_t)(b + u) * T + t;
+      g[u] = dres[row * C + c];
+      tok[u] = idx[row];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) one(b + u, g[u], tok[u]);
   }
+  for (; b < B; ++b) one(b, dres[((size_t)b * T + t) * C + c], idx[(size_t)b * T + t]);
   dwpe[i] += s;
 }
 
@@ -430,14 +429,10 @@ GPT2MI_EXPORT int gpt2mi_embed_bwd(const int64_t* idx, const float* dres, float*
                                    int T_valid, int C, float p, uint64_t seed, void* stream) {
   GPT2MI_REQUIRE(T_valid > 0 && T_valid <= T, "embed_bwd: T_valid=%d not in [1, T=%d]", T_valid, T);
   hipStream_t s = (hipStream_t)stream;
-  const int M = B * T;
   const uint32_t thr = drop_threshold(p);
   const float ik = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  embed_bwd_wte_kernel<<<grid_rows(M), 256, 0, s>>>(idx, dres, dwte, M, T, T_valid, C, seed, thr, ik);
-  int rc = gpt2mi::check_launch("embed_bwd_wte");
-  if (rc) return rc;
-  embed_bwd_wpe_kernel<<<(T_valid * C + 255) / 256, 256, 0, s>>>(dres, dwpe, B, T, T_valid, C, seed, thr, ik);
-  return gpt2mi::check_launch("embed_bwd_wpe");
+  embed_bwd_kernel<<<(T_valid * C + 255) / 256, 256, 0, s>>>(idx, dres, dwte, dwpe, B, T, T_valid, C, seed, thr, ik);
+  return gpt2mi::check_launch("embed_bwd");
 }
 
 template <typename TG>

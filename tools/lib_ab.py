@@ -59,6 +59,8 @@ def main():
         return adamw_mode(libs, g, st)
     if os.environ.get("LIB_AB_OP") == "xent":
         return xent_mode(libs, g, st)
+    if os.environ.get("LIB_AB_OP") == "embed":
+        return embed_mode(libs, g, st)
     outs = {}
     for i, lib in enumerate(libs):
         for name, (m, n, A, B, sp, ws) in data.items():
@@ -286,6 +288,36 @@ def xent_mode(libs, g, st):
     gb = 2 * 2 * M * ld / 1e9
     print("xent " + "  ".join(f"lib{i}: {sorted(t)[2] * 1e3:8.1f} us {gb / sorted(t)[2]:5.2f} TB/s"
                               for i, t in times.items()), flush=True)
+
+
+def embed_mode(libs, g, st):
+    """LIB_AB_OP=embed: the embedding backward at cfg 2 (B=64, T=1024, C=768, dropout 0.1): dwpe compared bitwise
+    against the first library, dwte (fp32 atomics, any order) to 1e-5."""
+    B, T, C, V = 64, 1024, 768, 50257
+    idx = torch.randint(0, V, (B * T,), device=dev, generator=g)
+    dres = torch.randn(B * T, C, device=dev, generator=g)
+    res = [(torch.zeros(V, C, device=dev), torch.zeros(T, C, device=dev)) for _ in libs]
+    run = lambda lib, r: lib.gpt2mi_embed_bwd(idx.data_ptr(), dres.data_ptr(), r[0].data_ptr(), r[1].data_ptr(),  # noqa
+                                              B, T, T, C, 0.1, 77, st)
+    for lib, r in zip(libs, res):
+        assert run(lib, r) == 0
+    torch.cuda.synchronize()
+    for i in range(1, len(libs)):
+        if not torch.equal(res[0][1], res[i][1]):
+            print(f"MISMATCH lib{i} dwpe")
+        if not torch.allclose(res[0][0], res[i][0], rtol=1e-5, atol=1e-6):
+            print(f"MISMATCH lib{i} dwte {(res[0][0] - res[i][0]).abs().max().item()}")
+    times = {i: [] for i in range(len(libs))}
+    for _ in range(5):
+        for i, (lib, r) in enumerate(zip(libs, res)):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _r in range(5):
+                run(lib, r)
+            e.record()
+            torch.cuda.synchronize()
+            times[i].append(s.elapsed_time(e) / 5)
+    print("embed_bwd " + "  ".join(f"lib{i}: {sorted(t)[2] * 1e3:8.1f} us" for i, t in times.items()), flush=True)
 
 
 if __name__ == "__main__":
