@@ -174,10 +174,15 @@ __device__ __forceinline__ f32x4 epilogue_apply(const GemmParams& P, int gm, int
 // epilogue's store tail is store-issue bound (per instruction, not per byte; cdna_hip_programming.md T21), so
 // half the instructions of the 4-wide form for the same bytes. Bitwise the same results as epilogue_apply.
 // r0 / r1: the primary output as stored (bf16-rounded), for fused column sums.
-__device__ __forceinline__ void store8_bf16(bf16* p, f32x4 a, f32x4 b) {
-  __builtin_nontemporal_store(bf16x8{f2bf(a[0]), f2bf(a[1]), f2bf(a[2]), f2bf(a[3]), f2bf(b[0]), f2bf(b[1]), f2bf(b[2]),
-                                     f2bf(b[3])},
-                              reinterpret_cast<bf16x8*>(p));
+// Returns the stored bf16 values: the as-stored column sums widen these bits instead of converting again.
+__device__ __forceinline__ bf16x8 store8_bf16(bf16* p, f32x4 a, f32x4 b) {
+  const bf16x8 v = {f2bf(a[0]), f2bf(a[1]), f2bf(a[2]), f2bf(a[3]), f2bf(b[0]), f2bf(b[1]), f2bf(b[2]), f2bf(b[3])};
+  __builtin_nontemporal_store(v, reinterpret_cast<bf16x8*>(p));
+  return v;
+}
+__device__ __forceinline__ void widen8(bf16x8 v, f32x4& r0, f32x4& r1) {
+  r0 = f32x4{bf2f(v[0]), bf2f(v[1]), bf2f(v[2]), bf2f(v[3])};
+  r1 = f32x4{bf2f(v[4]), bf2f(v[5]), bf2f(v[6]), bf2f(v[7])};
 }
 template <int EPI, int DROPM = -1>
 __device__ __forceinline__ void epilogue8(const GemmParams& P, int gm, int gn, f32x4 v0, f32x4 v1, bf16x8 op, f32x4& r0,
@@ -186,9 +191,7 @@ __device__ __forceinline__ void epilogue8(const GemmParams& P, int gm, int gn, f
   const bool drop = DROPM < 0 ? P.thr != 0u : DROPM == 1;
   bf16* C = reinterpret_cast<bf16*>(P.C) + (size_t)gm * P.ldc + gn;
   if constexpr (EPI == EPI_BF16) {
-    store8_bf16(C, v0, v1);
-    r0 = round4<bf16>(v0);
-    r1 = round4<bf16>(v1);
+    widen8(store8_bf16(C, v0, v1), r0, r1);
   } else if constexpr (EPI == EPI_GELU) {
     const uint32_t pidx = (uint32_t)gm * (uint32_t)(P.N >> 1) + (uint32_t)(gn >> 1);
     f32x4 h0, d0, h1, d1, m0 = {1.f, 1.f, 1.f, 1.f}, m1 = {1.f, 1.f, 1.f, 1.f};
@@ -203,15 +206,10 @@ __device__ __forceinline__ void epilogue8(const GemmParams& P, int gm, int gn, f
     r0 = h0;
     r1 = h1;
   } else {
-    f32x4 o0, o1;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      o0[j] = v0[j] * bf2f(op[j]);
-      o1[j] = v1[j] * bf2f(op[4 + j]);
-    }
-    store8_bf16(C, o0, o1);
-    r0 = round4<bf16>(o0);
-    r1 = round4<bf16>(o1);
+    // vector products: packed (v_pk_mul_f32) whether or not the compiler's SLP pass runs
+    const f32x4 o0 = v0 * f32x4{bf2f(op[0]), bf2f(op[1]), bf2f(op[2]), bf2f(op[3])};
+    const f32x4 o1 = v1 * f32x4{bf2f(op[4]), bf2f(op[5]), bf2f(op[6]), bf2f(op[7])};
+    widen8(store8_bf16(C, o0, o1), r0, r1);
   }
 }
 

@@ -490,12 +490,9 @@ write_image(mi, 0);
           bf16x8 op = {};
           if constexpr (EPI == EPI_GELU_BWD) op = op8[it];
           epilogue8<EPI, EPI == EPI_GELU ? VC : 0>(P, gm, gnb, w0, w1, op, r0, r1);
-          if constexpr (kCsum && VC == 1) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              csum[e] += r0[e];
-              csum1[e] += r1[e];
-            }
+          if constexpr (kCsum && VC == 1) {  // vector adds: packed (v_pk_add_f32) without SLP, see the Makefile
+            csum += r0;
+            csum1 += r1;
           }
         }
       };
@@ -547,10 +544,7 @@ write_image(mi, 0);
                                                          bf2f(opnd16[it][3])};
           else if constexpr (kOpnd) op = opnd[it];
           const f32x4 o = epilogue_apply<EPI, bf16, (EPI == EPI_RESID || EPI == EPI_GELU) ? VC : 0>(P, gm, gn, w, op);
-          if constexpr (kCsum && VC == 1) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) csum[e] += o[e];
-          }
+          if constexpr (kCsum && VC == 1) csum += o;
         }
       };
       const bool on = (EPI == EPI_RESID || EPI == EPI_GELU) ? P.thr != 0u : csum_on;
@@ -603,12 +597,9 @@ write_image(mi, wr * 64);
           bf16x8 op = {};
           if constexpr (EPI == EPI_GELU_BWD) op = op8[it];
           epilogue8<EPI, EPI == EPI_GELU ? VC : 0>(P, gm, gnb, w0, w1, op, r0, r1);
-          if constexpr (kCsum && VC == 1) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              csum[e] += r0[e];
-              csum1[e] += r1[e];
-            }
+          if constexpr (kCsum && VC == 1) {  // vector adds: packed (v_pk_add_f32) without SLP, see the Makefile
+            csum += r0;
+            csum1 += r1;
           }
         }
         }
@@ -657,10 +648,7 @@ write_image(mi, wr * 64);
         constexpr int DROPM = (EPI == EPI_RESID || EPI == EPI_GELU) ? VC : -1;
         const f32x4 o = epilogue_apply<EPI, bf16, DROPM>(P, gm, gn, v, kOpnd ? opnd[it] : f32x4{0.f, 0.f, 0.f, 0.f});
         if constexpr (kCsum) {
-          if (VC < 0 ? csum_on : VC == 1) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) csum[e] += o[e];
-          }
+          if (VC < 0 ? csum_on : VC == 1) csum += o;
         }
       }
     };

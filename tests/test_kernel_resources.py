@@ -44,7 +44,8 @@ def _resources(src, extra=()):
 @pytest.mark.skipif(not shutil.which(HIPCC) and not os.path.exists(HIPCC), reason="hipcc not available")
 @pytest.mark.parametrize("src", sorted(EXPECT))
 def test_no_scratch_and_occupancy(src):
-    extra = ("-fno-honor-nans", "-fno-slp-vectorize") if src == "attention.hip" else ()  # as the Makefile builds it
+    extra = {"attention.hip": ("-fno-honor-nans", "-fno-slp-vectorize"),  # as the Makefile builds them
+             "gemm_pp.hip": ("-fno-slp-vectorize",)}.get(src, ())
     kernels = _resources(src, extra)
     for sub, occ in EXPECT[src].items():
         found = {k: v for k, v in kernels.items() if sub in k}
