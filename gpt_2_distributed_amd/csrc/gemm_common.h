@@ -138,14 +138,12 @@ __device__ __forceinline__ f32x4 epilogue_apply(const GemmParams& P, int gm, int
     store4<float>(reinterpret_cast<float*>(P.C) + cidx, v);
   } else if constexpr (EPI == EPI_RESID) {
     // x + drop(y) rounded as two operations (the reference's dropout multiply, then the residual add): never
-    // contracted to an fma, so every kernel (and schedule) that applies this epilogue stores the same bits
-    if (drop) {
-      const f32x4 m = drop_scale4(P, pidx);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = __fmul_rn(v[j], m[j]);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) opnd[j] = __fadd_rn(opnd[j], v[j]);
+    // contracted to an fma, so every kernel (and schedule) that applies this epilogue stores the same bits. Vector
+    // operations: v_pk_mul_f32 / v_pk_add_f32 (two lanes' worth per instruction, each rounded on its own) whether
+    // or not the SLP pass runs (gemm_pp.hip is built without it)
+#pragma clang fp contract(off)
+    if (drop) v = v * drop_scale4(P, pidx);
+    opnd = opnd + v;
     store4<float>(reinterpret_cast<float*>(P.C) + cidx, opnd);
   } else if constexpr (EPI == EPI_GELU) {
     // the forward also emits what the backward needs of this site: dL/du = dL/dh * keep/(1-p) * gelu'(u),

@@ -481,11 +481,8 @@ write_image(mi, 0);
         for (int it = 0; it < 4; ++it) {
           const int gm = m0 + q * 64 + 16 * it + 2 * wid + hl;
           f32x4 w0 = va[it], w1 = vb[it];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            w0[e] += bias[e];
-            w1[e] += bias1[e];
-          }
+          w0 += bias;  // vector adds: packed without SLP
+          w1 += bias1;
           f32x4 r0, r1;
           bf16x8 op = {};
           if constexpr (EPI == EPI_GELU_BWD) op = op8[it];
@@ -537,8 +534,7 @@ write_image(mi, 0);
         for (int it = 0; it < 8; ++it) {
           const int gm = m0 + q * 64 + it * 8 + wid;
           f32x4 w = v[it];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) w[e] += bias[e];
+          w += bias;
           f32x4 op = {0.f, 0.f, 0.f, 0.f};
           if constexpr (EPI == EPI_GELU_BWD) op = f32x4{bf2f(opnd16[it][0]), bf2f(opnd16[it][1]), bf2f(opnd16[it][2]),
                                                          bf2f(opnd16[it][3])};
@@ -588,11 +584,8 @@ write_image(mi, wr * 64);
           const int gm = m0 + mi * 128 + 16 * it + 2 * wid + hl;
           if (GUARD && gm >= P.M) continue;
           f32x4 w0 = va[k], w1 = vb[k];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            w0[e] += bias[e];
-            w1[e] += bias1[e];
-          }
+          w0 += bias;  // vector adds: packed without SLP
+          w1 += bias1;
           f32x4 r0, r1;
           bf16x8 op = {};
           if constexpr (EPI == EPI_GELU_BWD) op = op8[it];
@@ -639,8 +632,7 @@ write_image(mi, wr * 64);
     auto finish = [&](int it, f32x4 v, auto vc) {
       constexpr int VC = decltype(vc)::value;
       const int gm = row_of(it);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] += bias[e];
+      v += bias;
       if constexpr (EPI == EPI_SLAB) {
         float* slab = reinterpret_cast<float*>(P.C) + (size_t)split * P.M * P.ldc;
         store4<float>(slab + (size_t)gm * P.ldc + gn, v);
