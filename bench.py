@@ -206,6 +206,8 @@ def main():
         "mfu": round(tok_s * fpt / (world * PEAK_BF16_TFLOPS * 1e12), 4),
         "flop_per_token": fpt,
         "final_loss": round(final_loss * GA, 4),
+        # peak HBM allocated on this rank (torch's caching allocator: activations, arenas, collective buffers)
+        "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 2),
         "roofline": roofline,
         "kernels": kernels,
         "cpu_baseline": None,

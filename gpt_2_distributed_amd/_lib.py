@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("GPT2MI_LIB") or os.path.join(_HERE, "libgpt2mi.so")
 
 # the ABI these bindings are written against (include/gpt2mi.h GPT2MI_ABI_VERSION): a stale or foreign
 # library is refused at load instead of being called with the wrong argument lists
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 _c_int, _c_float, _c_size, _c_u64, _p = ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_void_p
 
@@ -32,7 +32,7 @@ _SIGS = {
     "gpt2mi_layernorm_bwd": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_float, _c_u64, _c_int, _p],
     "gpt2mi_colsum_bf16": [_p, _p, _c_int, _c_int, _c_int, _p],
     "gpt2mi_gemm": [_c_int, _c_int, _c_int, _c_int, _c_int, _p, _c_int, _p, _c_int, _p, _c_int, _p, _p, _p, _c_int,
-                    _c_float, _p, _c_int, _c_int, _c_float, _c_u64, _p, _p],
+                    _c_float, _p, _c_int, _c_int, _c_float, _c_u64, _p, _c_int, _p],
     "gpt2mi_attn_fwd": [_p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_float, _c_u64, _p],
     "gpt2mi_attn_bwd": [_p, _p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_float, _c_u64, _p],
     "gpt2mi_xent_fwd": [_p, _c_int, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _p, _p, _p],
@@ -46,8 +46,6 @@ _SIGS = {
     "gpt2mi_scale_mul": [_p, _p, _p, _p],
     "gpt2mi_memset_zero": [_p, _c_size, _p],
     "gpt2mi_zero_ranges": [_p, _p, _c_int, _p],
-    "gpt2mi_set_gemm_impl": [_c_int],
-    "gpt2mi_set_gemm_persistent": [_c_int],
     "gpt2mi_gemm_f32": [_c_int, _c_int, _c_int, _c_int, _c_int, _p, _c_int, _p, _c_int, _p, _c_int, _p, _p, _p,
                         _c_int, _c_float, _p, _c_int, _c_int, _c_float, _c_u64, _p, _p],
     "gpt2mi_attn_fwd_f32": [_p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_float, _c_u64, _p],
@@ -66,9 +64,9 @@ _SIGS = {
     "gpt2mi_fsdp_pack": [_p, _p, _c_int, _c_size, _c_size, _p],
     "gpt2mi_fsdp_accum": [_p, _c_int, _p, _c_size, _c_int, _p],
     "gpt2mi_gemm_wgrad": [_c_int, _c_int, _c_int, _p, _c_int, _p, _c_int, _p, _c_int, _c_int, _c_float, _p, _p,
-                          _c_size, _c_int, _p],
+                          _c_size, _c_int, _c_int, _p],
 }
-_RESTYPES = {"gpt2mi_last_error": ctypes.c_char_p, "gpt2mi_set_gemm_impl": None, "gpt2mi_set_gemm_persistent": None}
+_RESTYPES = {"gpt2mi_last_error": ctypes.c_char_p}
 
 EXPORTED = tuple(_SIGS)
 
@@ -132,6 +130,9 @@ def _call(name: str, *args):
 # ---- typed wrappers ------------------------------------------------------------------------------
 EPI_BF16, EPI_F32, EPI_RESID, EPI_GELU, EPI_GELU_BWD, EPI_ATOMIC = range(6)
 FWD, DGRAD, WGRAD = 0, 1, 2
+# GEMM schedule per call (gpt2mi.h GPT2MI_SCHED_*): auto, or the flag that keeps the persistent schedule off while
+# RCCL kernels may share the CUs; the low byte picks a kernel for A/B experiments and kernel-equivalence tests
+SCHED_AUTO, SCHED_NO_PERSISTENT = 0, 0x100
 
 
 def embed_fwd(idx, wte, wpe, x, B, T, C, p=0.0, seed=0, T_valid=None):
@@ -163,17 +164,20 @@ def colsum_bf16(g, db, M, N, ld):
 
 
 def gemm(layout, epilogue, M, N, K, A, lda, B, ldb, C, ldc, bias=None, resid=None, aux=None, ldaux=0,
-         alpha=1.0, alpha_dev=None, accumulate=False, splits=1, p_drop=0.0, seed=0, dbias=None):
-    _call("gpt2mi_gemm_f32" if _f32(A) else "gpt2mi_gemm", layout, epilogue, M, N, K, _ptr(A), lda, _ptr(B), ldb, _ptr(C), ldc, _ptr(bias),
-          _ptr(resid), _ptr(aux), ldaux, alpha, _ptr(alpha_dev), int(accumulate), splits, p_drop, seed, _ptr(dbias),
-          _stream())
+         alpha=1.0, alpha_dev=None, accumulate=False, splits=1, p_drop=0.0, seed=0, dbias=None, sched=SCHED_AUTO):
+    args = (layout, epilogue, M, N, K, _ptr(A), lda, _ptr(B), ldb, _ptr(C), ldc, _ptr(bias), _ptr(resid), _ptr(aux),
+            ldaux, alpha, _ptr(alpha_dev), int(accumulate), splits, p_drop, seed, _ptr(dbias))
+    if _f32(A):  # the fp32 kernels have one schedule
+        _call("gpt2mi_gemm_f32", *args, _stream())
+    else:
+        _call("gpt2mi_gemm", *args, int(sched), _stream())
 
 
 def gemm_wgrad(M, N, K, A, lda, B, ldb, C, ldc, accumulate=True, alpha=1.0, alpha_dev=None, workspace=None,
-               splits=1):
+               splits=1, sched=SCHED_AUTO):
     ws_n = workspace.numel() if workspace is not None else 0
     _call("gpt2mi_gemm_wgrad", M, N, K, _ptr(A), lda, _ptr(B), ldb, _ptr(C), ldc, int(accumulate), alpha,
-          _ptr(alpha_dev), _ptr(workspace), ws_n, splits, _stream())
+          _ptr(alpha_dev), _ptr(workspace), ws_n, splits, int(sched), _stream())
 
 
 def wgrad_splits(M, N, K, cus=256):
@@ -183,7 +187,7 @@ def wgrad_splits(M, N, K, cus=256):
     blocks is not mostly idle: the tied lm_head wgrad (197 x 3 = 591 tiles = 2.3 rounds) runs as 3
     splits (1773 blocks = 6.9 rounds of 1/3 the depth); the small block wgrads fill one round.
     Each split keeps >= 4 K-tiles of 64."""
-    tiles = (M // 256) * (N // 256)
+    tiles = -(-M // 256) * -(-N // 256)  # (a partial last tile counts as a tile)
     if tiles == 0:
         return 1
     best, best_cost = 1, None
@@ -285,13 +289,3 @@ def zero_ranges(t: torch.Tensor, ranges: torch.Tensor):
     """Zero the element ranges of fp32 t given as a cuda int64 [n, 2] tensor of (offset, count)."""
     assert t.dtype == torch.float32 and ranges.dtype == torch.int64 and ranges.is_cuda
     _call("gpt2mi_zero_ranges", _ptr(t), _ptr(ranges), ranges.shape[0], _stream())
-
-
-def set_gemm_impl(impl: int):
-    """0 = auto (256x256 kernel where it applies), 1 = force the 128x128 kernel (A/B benchmarking)."""
-    load().gpt2mi_set_gemm_impl(impl)
-
-
-def set_gemm_persistent(on: bool):
-    """Allow (default) or forbid the persistent GEMM schedule in the auto selection (gpt2mi.h)."""
-    load().gpt2mi_set_gemm_persistent(int(bool(on)))

@@ -306,8 +306,8 @@ __global__ __launch_bounds__(kThreads, ATTN_FWD_OCC) void attn_fwd_kernel(const 
 #pragma unroll
           for (int d = 0; d < 4; ++d) {  // dword d: keys (fi, r), (fi, r + 1) with fi = 2kk + (d >> 1), r = 2(d & 1)
             const uint32_t c = 16 * (2 * kk + (d >> 1)) + 2 * (d & 1);
-            const uint32_t ka = drop_keep_mask2(tk2, drop_fin(pre + c * kDropC1));
-            const uint32_t kb = drop_keep_mask2(tk2, drop_fin(pre + (c + 1) * kDropC1));
+            const uint32_t ka = drop_keep_mask2(tk2, drop_fin(pre + c * kDropC1, seed_kx(seed)));
+            const uint32_t kb = drop_keep_mask2(tk2, drop_fin(pre + (c + 1) * kDropC1, seed_kx(seed)));
             // the bytes of each bf16 = the sign (keep bit) of key r's / key r+1's decision for query group 0 / 1
             w0[d] &= __builtin_amdgcn_perm(kb, ka, 0x0A0A0808u);
             w1[d] &= __builtin_amdgcn_perm(kb, ka, 0x0B0B0909u);
@@ -440,7 +440,7 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const bf16* __
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             uint32_t hh = 0;
-            if constexpr (DROP) hh = drop_fin(pre + (uint32_t)(16 * fi + r) * kDropC1);
+            if constexpr (DROP) hh = drop_fin(pre + (uint32_t)(16 * fi + r) * kDropC1, seed_kx(seed));
 #pragma unroll
             for (int qg = 0; qg < 2; ++qg) {
               float p = __builtin_amdgcn_exp2f(fmaf(s[qg][fi][r], sl2, -lse2[qg]));
@@ -597,7 +597,7 @@ __global__ __launch_bounds__(64 * kDkdvWaves) __attribute__((amdgpu_waves_per_eu
             for (int r = 0; r < 4; ++r) {
               uint32_t hh = 0;  // queries q and q^16 (fl = 0, 1) share one dropout hash
               // counter (bh*T + q0 + 4g + 32hq + r) * T + key: a lane base plus (32hq + r) * T + 16kg (uniform)
-              if constexpr (DROP) hh = drop_fin(pre_t + ((uint32_t)(32 * hq + r) * (uint32_t)T + 16u * kg) * kDropC1);
+              if constexpr (DROP) hh = drop_fin(pre_t + ((uint32_t)(32 * hq + r) * (uint32_t)T + 16u * kg) * kDropC1, seed_kx(seed));
 #pragma unroll
               for (int fl = 0; fl < 2; ++fl) {
                 float p = __builtin_amdgcn_exp2f(fmaf(s[kg][fl][r], sl2, -l4[fl][r]));

@@ -54,21 +54,35 @@ __device__ __forceinline__ float wave_max(float v) {
 // share a hash (GEMM/LN/embedding sites: elements 2j, 2j+1; attention: queries q, q^16 of one key,
 // which sit in the same lane in every attention kernel). keep = int16(uniform16) >= round(p * 2^16) - 2^15.
 // All element / pair indices fit in 32 bits for every BASELINE config (attention B*H*T*T < 2^32).
-__device__ __forceinline__ uint32_t seed32(uint64_t seed) { return (uint32_t)seed ^ (uint32_t)(seed >> 32); }
+// The 64-bit site seed holds two words: s32 (low) enters the first round additively, the odd multiplier of the
+// second round is the high word (a vetted per-site constant, gpt_2_distributed_amd/dropout_keys.py). With one
+// multiplier for every site, each site's mask would be a translate of ONE 2^32-long sequence (site s at counter x =
+// site s' at x + s - s'), and a step draws ~6.7e9 counters at cfg 2, so sites would reuse each other's decisions;
+// distinct multipliers make the sites' sequences distinct functions (tests/test_oracle.py: decision correlation
+// between sites at equal and shifted counters). Free: the multiply takes an SGPR instead of a literal.
+__device__ __forceinline__ uint32_t seed32(uint64_t seed) { return (uint32_t)seed; }
+// (a seed with a zero high word, e.g. a small integer, takes murmur3's 0x85EBCA6B)
+constexpr uint32_t kDropC2 = 0x85EBCA6Bu;
+__device__ __forceinline__ uint32_t seed_kx(uint64_t seed) {
+  const uint32_t hi = (uint32_t)(seed >> 32);
+  return hi ? hi | 1u : kDropC2;
+}
 // Two rounds of multiply-xorshift (murmur3 fmix32 without its closing rounds). The first round is linear in the
 // counter, (x + s32) * C1, so a kernel walking counters x + c (c a per-element constant) forms it as
 // drop_pre(s32, x) + c * C1: one v_add instead of an add, xor and v_mul_lo_u32 (half the VALU rate, measured by
 // tools/valu_probe.hip) per hash.
-constexpr uint32_t kDropC1 = 0x9E3779B1u, kDropC2 = 0x85EBCA6Bu;
+constexpr uint32_t kDropC1 = 0x9E3779B1u;
 __device__ __forceinline__ uint32_t drop_pre(uint32_t s32, uint32_t x) { return (x + s32) * kDropC1; }
-// The second round ends at the multiply: a closing xorshift (murmur3's h ^= h >> 13) leaves the 16-bit decisions
-// statistically unchanged (tests/test_oracle.py: decision correlations over the kernels' counter strides) and
-// costs three instructions per hash in the attention kernels.
-__device__ __forceinline__ uint32_t drop_fin(uint32_t h) {
+// The second round ends at the multiply (by the site's multiplier kx): a closing xorshift (murmur3's h ^= h >> 13)
+// leaves the 16-bit decisions statistically unchanged (tests/test_oracle.py: decision correlations over the
+// kernels' counter strides) and costs three instructions per hash in the attention kernels.
+__device__ __forceinline__ uint32_t drop_fin(uint32_t h, uint32_t kx) {
   h ^= h >> 16;
-  return h * kDropC2;
+  return h * kx;
 }
-__device__ __forceinline__ uint32_t drop_hash(uint32_t s32, uint32_t x) { return drop_fin(drop_pre(s32, x)); }
+__device__ __forceinline__ uint32_t drop_hash(uint32_t s32, uint32_t kx, uint32_t x) {
+  return drop_fin(drop_pre(s32, x), kx);
+}
 // keep iff the 16-bit half, read as a signed int16, is >= thr - 32768 (P(keep) = 1 - thr / 2^16): a signed
 // threshold, so packed-int16 arithmetic can form the decisions of a pair at once from the sign bits of
 // (thr - 32769) -sat- half (drop_keep_mask2)
@@ -89,7 +103,7 @@ __device__ __forceinline__ uint32_t drop_keep_mask2(uint32_t tk2, uint32_t h) {
 }
 // element-indexed form: element i uses half (i & 1) of hash(i >> 1)
 __device__ __forceinline__ bool drop_keep(uint64_t seed, uint64_t idx, uint32_t thr) {
-  return drop_keep16(drop_hash(seed32(seed), (uint32_t)(idx >> 1)), (int)(idx & 1), thr);
+  return drop_keep16(drop_hash(seed32(seed), seed_kx(seed), (uint32_t)(idx >> 1)), (int)(idx & 1), thr);
 }
 
 static inline uint32_t drop_threshold(float p) {

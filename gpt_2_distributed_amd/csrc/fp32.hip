@@ -147,8 +147,8 @@ constexpr int HD = 64;       // head dim
 constexpr int RT = 64;       // rows (queries or keys) per tile / per workgroup
 constexpr int kAThreads = 256;  // 4 lanes per row
 
-__device__ __forceinline__ bool attn_keep(uint32_t s32, int bh, int T, int q, int key, uint32_t thr) {
-  const uint32_t hh = drop_hash(s32, ((uint32_t)bh * T + (q & ~16)) * (uint32_t)T + key);
+__device__ __forceinline__ bool attn_keep(uint32_t s32, uint32_t kx, int bh, int T, int q, int key, uint32_t thr) {
+  const uint32_t hh = drop_hash(s32, kx, ((uint32_t)bh * T + (q & ~16)) * (uint32_t)T + key);
   return drop_keep16(hh, (q >> 4) & 1, thr);
 }
 
@@ -194,7 +194,7 @@ __global__ __launch_bounds__(kAThreads) void attn_fwd_f32_kernel(const float* __
   const float* base = qkv + (size_t)b * T * ld;
   const int r = threadIdx.x >> 2, qd = threadIdx.x & 3;
   const int q = qt * RT + r;
-  const uint32_t s32 = seed32(seed);
+  const uint32_t s32 = seed32(seed), kx = seed_kx(seed);
   float qv[16], acc[16];
   ld16(qv, base + (size_t)q * ld + h * HD + 16 * qd);
 #pragma unroll
@@ -231,7 +231,7 @@ __global__ __launch_bounds__(kAThreads) void attn_fwd_f32_kernel(const float* __
       for (int j = 0; j < 16; ++j) {
         float p = __expf(s[j] - mn);
         l += p;
-        if (thr) p = attn_keep(s32, bh, T, q, kt * RT + jc + j, thr) ? p * inv_keep : 0.f;
+        if (thr) p = attn_keep(s32, kx, bh, T, q, kt * RT + jc + j, thr) ? p * inv_keep : 0.f;
         const float* vr = kv[1] + (jc + j) * HD + 16 * qd;
 #pragma unroll
         for (int d = 0; d < 16; ++d) acc[d] += p * vr[d];
@@ -269,7 +269,7 @@ __global__ __launch_bounds__(kAThreads) void attn_bwd_dkdv_f32_kernel(
   const float* dbase = dout + (size_t)b * T * C;
   const int r = threadIdx.x >> 2, qd = threadIdx.x & 3;
   const int key = kt * RT + r;
-  const uint32_t s32 = seed32(seed);
+  const uint32_t s32 = seed32(seed), kx = seed_kx(seed);
   float kr[16], vr[16], dk[16], dv[16];
   ld16(kr, base + (size_t)key * ld + C + h * HD + 16 * qd);
   ld16(vr, base + (size_t)key * ld + 2 * C + h * HD + 16 * qd);
@@ -302,7 +302,7 @@ __global__ __launch_bounds__(kAThreads) void attn_bwd_dkdv_f32_kernel(
       const float p = __expf(s - sl[i]);
       float pd = p;
       if (thr) {
-        const bool keep = attn_keep(s32, bh, T, q, key, thr);
+        const bool keep = attn_keep(s32, kx, bh, T, q, key, thr);
         pd = keep ? p * inv_keep : 0.f;
         dp = keep ? dp * inv_keep : 0.f;
       }
@@ -331,7 +331,7 @@ __global__ __launch_bounds__(kAThreads) void attn_bwd_dq_f32_kernel(
   const float* base = qkv + (size_t)b * T * ld;
   const int r = threadIdx.x >> 2, qd = threadIdx.x & 3;
   const int q = qt * RT + r;
-  const uint32_t s32 = seed32(seed);
+  const uint32_t s32 = seed32(seed), kx = seed_kx(seed);
   float qv[16], gv[16], dq[16];
   ld16(qv, base + (size_t)q * ld + h * HD + 16 * qd);
   ld16(gv, dout + ((size_t)b * T + q) * C + h * HD + 16 * qd);
@@ -358,7 +358,7 @@ __global__ __launch_bounds__(kAThreads) void attn_bwd_dq_f32_kernel(
       s = quad_sum(s) * scale;
       dp = quad_sum(dp);
       const float p = __expf(s - lq);
-      if (thr) dp = attn_keep(s32, bh, T, q, key, thr) ? dp * inv_keep : 0.f;
+      if (thr) dp = attn_keep(s32, kx, bh, T, q, key, thr) ? dp * inv_keep : 0.f;
       const float ds = p * (dp - dl) * scale;
 #pragma unroll
       for (int d = 0; d < 16; ++d) dq[d] += ds * kr[d];

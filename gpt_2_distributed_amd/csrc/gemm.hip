@@ -209,22 +209,11 @@ int launch(const GemmParams& P, int splits, hipStream_t s) {
 
 }  // namespace
 
-// 0 auto (ping-pong 256x256, persistent for short K), 1 force 128x128, 2 force the 2-stage 256x256, 3..5
-// ping-pong with half-tile map 1..3, 6 ping-pong without the persistent schedule, 7 persistent at any K,
-// 8 = 0 for the weight gradients, 9 the ring wgrad kernel (2 / 9: the weight gradients on gemm256)
-// (A/B experiments, tools/gemm_probe.py, tools/gemm_ab.py)
-static int g_gemm_impl = 0;
-GPT2MI_EXPORT void gpt2mi_set_gemm_impl(int impl) { g_gemm_impl = impl; }
-namespace gpt2mi {
-bool g_gemm_persistent = true;
-}
-GPT2MI_EXPORT void gpt2mi_set_gemm_persistent(int on) { gpt2mi::g_gemm_persistent = on != 0; }
-
 // layout: 0 = forward (A[M][K], B[N][K]); 1 = dgrad (A[M][K], B[K][N]); 2 = wgrad (A[K][M], B[K][N]).
 GPT2MI_EXPORT int gpt2mi_gemm(int layout, int epilogue, int M, int N, int K, const uint16_t* A, int lda,
                               const uint16_t* B, int ldb, void* C, int ldc, const float* bias, const float* resid,
                               uint16_t* aux, int ldaux, float alpha, const float* alpha_dev, int accumulate,
-                              int splits, float p_drop, uint64_t seed, float* dbias, void* stream) {
+                              int splits, float p_drop, uint64_t seed, float* dbias, int sched, void* stream) {
   GPT2MI_REQUIRE(dbias == nullptr || ((epilogue == EPI_BF16 || epilogue == EPI_GELU_BWD) && layout <= 1),
                  "gemm: dbias (fused column sum) needs the BF16 or GELU_BWD epilogue of layout 0/1");
   // 128-wide tiles with a half-width last tile in N (and in M for the transposed A of wgrad): C = 1600
@@ -234,6 +223,9 @@ GPT2MI_EXPORT int gpt2mi_gemm(int layout, int epilogue, int M, int N, int K, con
                  splits);
   GPT2MI_REQUIRE(splits == 1 || epilogue == EPI_ATOMIC, "gemm: split-K needs the atomic epilogue");
   GPT2MI_REQUIRE(layout >= 0 && layout <= 2, "gemm: bad layout %d", layout);
+  GPT2MI_REQUIRE((sched & ~(GPT2MI_SCHED_NO_PERSISTENT | 0xff)) == 0 && (sched & 0xff) <= 8, "gemm: bad sched %#x",
+                 sched);
+  const int impl = sched & 0xff;
   GPT2MI_REQUIRE(ldc % 4 == 0 && (ldaux % 4 == 0 || aux == nullptr), "gemm: ldc/ldaux must be multiples of 4");
   GPT2MI_REQUIRE(p_drop <= 0.f || (size_t)M * N < (1ull << 33),
                  "gemm: M*N=%zu exceeds the 32-bit dropout pair index", (size_t)M * N);
@@ -255,21 +247,27 @@ GPT2MI_EXPORT int gpt2mi_gemm(int layout, int epilogue, int M, int N, int K, con
   P.thr = drop_threshold(p_drop);
   P.inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
   hipStream_t s = (hipStream_t)stream;
-  const bool big_ok = splits == 1 && N % 256 == 0 && epilogue != EPI_ATOMIC && (layout <= 1 || M % 256 == 0);
-  if (big_ok && (g_gemm_impl == 0 || g_gemm_impl >= 3)) {
+  // the ping-pong kernel takes any M, N multiple of 64 (a partial last tile; GPT-2 1.5B's 1600 / 4800) and any K-tile
+  // count >= 2; the 2-stage 256x256 kernel full column tiles only
+  // (transposed operands — layouts 1 / 2 — full tiles only: the partial-tile reads of an m-contiguous operand run
+  // past its rows, which gpt2mi_gemm_wgrad's callers allocate for and this entry's do not)
+  const bool pp_ok = splits == 1 && epilogue != EPI_ATOMIC &&
+                     (layout == 0 || (N % 256 == 0 && (layout == 1 || M % 256 == 0)));
+  const bool big_ok = pp_ok && N % 256 == 0 && (layout <= 1 || M % 256 == 0);
+  if (pp_ok && (impl == 0 || impl >= 3)) {
     // impl 6: the ping-pong kernel without its persistent schedule (A/B)
-    const int map = g_gemm_impl == 6 ? -1 : g_gemm_impl == 7 ? 7 : g_gemm_impl >= 3 ? g_gemm_impl - 2 : 0;
-    const int rc = gpt2mi::gemm_pp_dispatch(layout, epilogue, P, s, 1, map);
+    const int map = impl == 6 ? -1 : impl == 7 ? 7 : (impl >= 3 && impl <= 5) ? impl - 2 : 0;
+    const int rc = gpt2mi::gemm_pp_dispatch(layout, epilogue, P, s, 1, map, !(sched & GPT2MI_SCHED_NO_PERSISTENT));
     if (rc >= 0) return rc;  // the ping-pong kernel fuses dbias
   }
   if (dbias) {  // other kernels: the GEMM, then the column sums of its output
     P.dbias = nullptr;
     const int rc = gpt2mi_gemm(layout, epilogue, M, N, K, A, lda, B, ldb, C, ldc, bias, resid, aux, ldaux, alpha,
-                               alpha_dev, accumulate, splits, p_drop, seed, nullptr, stream);
+                               alpha_dev, accumulate, splits, p_drop, seed, nullptr, sched, stream);
     if (rc) return rc;
     return gpt2mi_colsum_bf16((const uint16_t*)C, dbias, M, N, ldc, stream);
   }
-  if (big_ok && g_gemm_impl != 1) {
+  if (big_ok && impl != 1) {
     const int rc = gpt2mi::gemm256_dispatch(layout, epilogue, P, s, 1);
     if (rc >= 0) return rc;
   }
@@ -295,11 +293,15 @@ GPT2MI_EXPORT int gpt2mi_gemm(int layout, int epilogue, int M, int N, int K, con
 // (splits*M*N floats), then one pass sums them in fixed order into C (deterministic; no atomics).
 GPT2MI_EXPORT int gpt2mi_gemm_wgrad(int M, int N, int K, const uint16_t* A, int lda, const uint16_t* B, int ldb,
                                     float* C, int ldc, int accumulate, float alpha, const float* alpha_dev,
-                                    float* workspace, size_t workspace_floats, int splits, void* stream) {
-  GPT2MI_REQUIRE(M % 256 == 0 && N % 256 == 0 && K % 64 == 0, "gemm_wgrad: M=%d N=%d must be multiples of 256, K=%d of 64",
-                 M, N, K);
+                                    float* workspace, size_t workspace_floats, int splits, int sched,
+                                    void* stream) {
+  GPT2MI_REQUIRE(M % 64 == 0 && N % 64 == 0 && K % 64 == 0 && M > 0 && N > 0 && K > 0,
+                 "gemm_wgrad: M=%d N=%d K=%d must be multiples of 64", M, N, K);
   GPT2MI_REQUIRE(ldc == N, "gemm_wgrad: C must be dense (ldc == N)");
   GPT2MI_REQUIRE(splits >= 1 && splits <= K / 64, "gemm_wgrad: bad splits %d", splits);
+  GPT2MI_REQUIRE((sched & ~(GPT2MI_SCHED_NO_PERSISTENT | 0xff)) == 0 && (sched & 0xff) <= 8, "gemm_wgrad: bad sched %#x",
+                 sched);
+  const int impl = sched & 0xff;  // 2: the 2-stage 256x256 kernel (A/B); 0 / 8: the ping-pong kernel
   hipStream_t s = (hipStream_t)stream;
   GemmParams P{};
   P.A = (const bf16*)A;
@@ -311,7 +313,12 @@ GPT2MI_EXPORT int gpt2mi_gemm_wgrad(int M, int N, int K, const uint16_t* A, int 
   const int ktiles = K / 64;
   // the ping-pong kernel (default; impl 8) walks K-tile pairs: an even tile count per split (the last split's
   // count is then even too when ktiles is)
-  const bool pp = (g_gemm_impl == 0 || g_gemm_impl == 8) && ktiles % 2 == 0;
+  const bool pp = (impl == 0 || impl == 8) && ktiles % 2 == 0;
+  if (!pp && (M % 256 != 0 || N % 256 != 0 || impl == 1)) {
+    // an odd token-tile count with a partial output tile: the 128x128 kernel (accumulates into / writes C, one pass)
+    return gpt2mi_gemm(2, EPI_F32, M, N, K, A, lda, B, ldb, C, ldc, nullptr, nullptr, nullptr, 0, alpha, alpha_dev,
+                       accumulate, 1, 0.f, 0, nullptr, GPT2MI_SCHED_AUTO, stream);
+  }
   int tiles_per = (ktiles + splits - 1) / splits;
   if (pp) tiles_per += tiles_per & 1;
   P.k_per_split = tiles_per * 64;
@@ -319,17 +326,17 @@ GPT2MI_EXPORT int gpt2mi_gemm_wgrad(int M, int N, int K, const uint16_t* A, int 
   if (splits == 1) {
     P.C = C;
     if (pp) {
-      const int rc = gpt2mi::gemm_pp_dispatch(2, EPI_F32, P, s, 1, g_gemm_impl);
+      const int rc = gpt2mi::gemm_pp_dispatch(2, EPI_F32, P, s, 1, 0);
       if (rc >= 0) return rc;
     }
-    return gpt2mi::gemm256_dispatch(2, EPI_F32, P, s, 1, g_gemm_impl == 9);
+    return gpt2mi::gemm256_dispatch(2, EPI_F32, P, s, 1);
   }
   GPT2MI_REQUIRE(workspace != nullptr && workspace_floats >= (size_t)splits * M * N,
                  "gemm_wgrad: workspace of %zu floats < splits*M*N = %zu", workspace_floats, (size_t)splits * M * N);
   P.C = workspace;
   P.accumulate = 0;
-  int rc = pp ? gpt2mi::gemm_pp_dispatch(2, EPI_SLAB, P, s, splits, g_gemm_impl) : -1;
-  if (rc < 0) rc = gpt2mi::gemm256_dispatch(2, EPI_SLAB, P, s, splits, g_gemm_impl == 9);
+  int rc = pp ? gpt2mi::gemm_pp_dispatch(2, EPI_SLAB, P, s, splits, 0) : -1;
+  if (rc < 0) rc = gpt2mi::gemm256_dispatch(2, EPI_SLAB, P, s, splits);
   if (rc) return rc;
   return gpt2mi::splitk_reduce(workspace, splits, (size_t)M * N, C, accumulate, s);
 }

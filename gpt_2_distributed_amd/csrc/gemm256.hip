@@ -246,143 +246,6 @@ __global__ __launch_bounds__(kThreads, 1) void gemm256_kernel(GemmParams P) {
   }
 }
 
-// ---- weight gradients on a 5-slot ring of 32-deep half K-tiles (WG_RING) --------------------------------------
-// Same 256x256 tile, wave tiles, fragments and register epilogue as gemm256_kernel<true, true>, but the LDS
-// (all 160 KiB) is a ring of five 32 KiB slots, each one 32-deep half K-tile of both operands ([32][256]
-// m-contiguous images, the mc swizzle). One barrier per 64-deep K-tile as before; at the start of K-tile kt
-// the halves 2kt+3 and 2kt+4 are issued into the slots K-tile kt-1 just released, and the wait at its end
-// retires only what K-tile kt+1 reads (vmcnt(4): half 2kt+4 stays in flight across the barrier). Three
-// halves (96 KiB per CU) are in flight during the MFMAs instead of one K-tile (64 KiB) that must land by the
-// barrier: the 2-stage kernel's L2->LDS operand feed ran at the rate of one 64 KiB round trip per K-tile
-// (tools/wgrad_ablation.sh: DMA alone 3.19 of its 5.19 ms on the lm_head shape).
-constexpr int kSlot = 32 * 1024;
-constexpr int kSlots = 5;
-
-__device__ __forceinline__ uint32_t ring_lane_off(int ld, int wid, int t, int lane) {
-  const int k = 8 * ((wid >> 1) & 1) + 2 * t + (lane >> 5);  // k-row (mod 16) of instruction wid * 2 + t
-  return (uint32_t)(((lane >> 5) * ld + 8 * ((lane & 31) ^ mc_swz(k))) * (int)sizeof(bf16));
-}
-// one operand's 32-deep half: 16 x 1 KiB buffer LDS-DMA instructions (2 k-rows of 512 B each), 2 per wave
-__device__ __forceinline__ void dma_half_mc(const bf16* __restrict__ src, int ld, int row0, int k0,
-                                            const uint32_t (&loff)[2], char* dst, int wid) {
-  const u32x4 rs = buf_desc(src + (size_t)k0 * ld);
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int ins = wid * 2 + t;
-    const int soff = ((2 * ins) * ld + row0) * (int)sizeof(bf16);
-    lds_dma16_buf(rs, loff[t], soff, dst + ins * 1024);
-  }
-}
-
-template <int EPI>
-__global__ __launch_bounds__(kThreads, 1) void wgrad_ring_kernel(GemmParams P) {
-  __shared__ __attribute__((aligned(1024))) char smem[kSlots * kSlot];
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wid >> 2, wn = wid & 3;
-
-  const int tiles_m = P.M / BM, tiles_n = P.N / BN;
-  const int ntiles = tiles_m * tiles_n;
-  const int nsplit = (P.K + P.k_per_split - 1) / P.k_per_split;
-  const int item = xcd_remap(blockIdx.x, ntiles * nsplit);
-  const int split = item / ntiles;
-  const int pid = item - split * ntiles;
-  constexpr int GM = 4;
-  const int group = pid / (GM * tiles_n);
-  const int first_m = group * GM;
-  const int gsz = min(tiles_m - first_m, GM);
-  const int m0 = (first_m + (pid % (GM * tiles_n)) % gsz) * BM;
-  const int n0 = ((pid % (GM * tiles_n)) / gsz) * BN;
-  const int kbeg = split * P.k_per_split;
-  const int nk = (min(P.K, kbeg + P.k_per_split) - kbeg) / BK;
-  const int nh = 2 * nk;
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const uint32_t loff_a[2] = {ring_lane_off(P.lda, wid, 0, lane), ring_lane_off(P.lda, wid, 1, lane)};
-  const uint32_t loff_b[2] = {ring_lane_off(P.ldb, wid, 0, lane), ring_lane_off(P.ldb, wid, 1, lane)};
-  auto issue = [&](int h, int slot) {  // half h (32 k-rows) of this split into ring slot `slot`
-    char* dst = smem + slot * kSlot;
-    dma_half_mc(P.A, P.lda, m0, kbeg + 32 * h, loff_a, dst, wid);
-    dma_half_mc(P.B, P.ldb, n0, kbeg + 32 * h, loff_b, dst + kSlot / 2, wid);
-  };
-  issue(0, 0);
-  issue(1, 1);
-  if (nh > 2) {
-    issue(2, 2);
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __builtin_amdgcn_s_barrier();
-
-  int slot = 0;  // ring slot of half 2kt
-  for (int kt = 0; kt < nk; ++kt) {
-    const int h3 = 2 * kt + 3;
-    int s3 = slot + 3, s4 = slot + 4;
-    s3 -= s3 >= kSlots ? kSlots : 0;
-    s4 -= s4 >= kSlots ? kSlots : 0;
-    if (h3 < nh) issue(h3, s3);
-    if (h3 + 1 < nh) issue(h3 + 1, s4);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      int sk = slot + kk;
-      sk -= sk >= kSlots ? kSlots : 0;
-      const char* As = smem + sk * kSlot;
-      const char* Bs = As + kSlot / 2;
-      bf16x8 bf[4], af[8];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bf[j] = frag_mc(Bs, 0, wn * 64 + 16 * j, lane);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) af[i] = frag_mc(As, 0, wm * 128 + 16 * i, lane);
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[i][j], 0, 0, 0);
-    }
-    if (kt + 1 < nk) {  // halves 2kt+2, 2kt+3 (K-tile kt+1) landed; 2kt+4, if issued, stays in flight
-      if (h3 + 1 < nh) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-    }
-    slot += 2;
-    slot -= slot >= kSlots ? kSlots : 0;
-  }
-
-  float alpha = P.alpha;
-  if (P.alpha_dev) alpha *= P.alpha_dev[0];
-  const int gcol0 = n0 + wn * 64 + 4 * (lane >> 4);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int gm = m0 + wm * 128 + 16 * i + (lane & 15);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int gn = gcol0 + 16 * j;
-      f32x4 v;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * alpha;
-      if constexpr (EPI == EPI_SLAB) {
-        float* slab = reinterpret_cast<float*>(P.C) + (size_t)split * P.M * P.ldc;
-        *reinterpret_cast<f32x4*>(slab + (size_t)gm * P.ldc + gn) = v;
-      } else {
-        epilogue_store<EPI>(P, gm, gn, v);
-      }
-    }
-  }
-}
-
-template <int EPI>
-int launch_ring(const GemmParams& P, hipStream_t s, int splits) {
-  dim3 grid((P.M / BM) * (P.N / BN) * splits);
-  wgrad_ring_kernel<EPI><<<grid, kThreads, 0, s>>>(P);
-  return gpt2mi::check_launch("gemm256_wgrad_ring");
-}
-
 template <bool A_T, bool B_T, int EPI>
 int launch(const GemmParams& P, hipStream_t s, int splits) {
   dim3 grid(((P.M + BM - 1) / BM) * (P.N / BN) * splits);
@@ -407,7 +270,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 
 namespace gpt2mi {
 // Layouts 0 (forward) and 1 (dgrad); N % 256 == 0, M % 64 == 0, K % 32 == 0, no split-K.
-int gemm256_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t s, int splits, bool ring) {
+int gemm256_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t s, int splits) {
   switch (layout * 16 + epilogue) {
     case 0 * 16 + EPI_BF16: return launch<false, false, EPI_BF16>(P, s, 1);
     case 0 * 16 + EPI_F32: return launch<false, false, EPI_F32>(P, s, 1);
@@ -417,10 +280,8 @@ int gemm256_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t 
     case 1 * 16 + EPI_BF16: return launch<false, true, EPI_BF16>(P, s, 1);
     case 1 * 16 + EPI_F32: return launch<false, true, EPI_F32>(P, s, 1);
     case 1 * 16 + EPI_GELU_BWD: return launch<false, true, EPI_GELU_BWD>(P, s, 1);
-    case 2 * 16 + EPI_F32:
-      return (ring && P.M % BM == 0) ? launch_ring<EPI_F32>(P, s, 1) : launch<true, true, EPI_F32>(P, s, 1);
-    case 2 * 16 + EPI_SLAB:
-      return (ring && P.M % BM == 0) ? launch_ring<EPI_SLAB>(P, s, splits) : launch<true, true, EPI_SLAB>(P, s, splits);
+    case 2 * 16 + EPI_F32: return launch<true, true, EPI_F32>(P, s, 1);
+    case 2 * 16 + EPI_SLAB: return launch<true, true, EPI_SLAB>(P, s, splits);
     default: return -1;  // not built for this kernel: caller falls back to the 128x128 kernel
   }
 }

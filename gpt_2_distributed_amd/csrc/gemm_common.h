@@ -34,9 +34,9 @@ struct GemmParams {
 // keep mask of the 4 dropout elements 2*pidx .. 2*pidx+3 as multipliers keep/(1-p) or 0 (x * m is the
 // dropout of x, as torch's fused dropout forms it): two hashes, 16 bits per element
 __device__ __forceinline__ f32x4 drop_scale4(const GemmParams& P, uint32_t pidx) {
-  const uint32_t s = seed32(P.seed);
+  const uint32_t s = seed32(P.seed), kx = seed_kx(P.seed);
   const uint32_t pre = drop_pre(s, pidx);
-  const uint32_t h0 = drop_fin(pre), h1 = drop_fin(pre + kDropC1);
+  const uint32_t h0 = drop_fin(pre, kx), h1 = drop_fin(pre + kDropC1, kx);
   const float k = P.inv_keep;
   return f32x4{drop_keep16(h0, 0, P.thr) ? k : 0.f, drop_keep16(h0, 1, P.thr) ? k : 0.f,
                drop_keep16(h1, 0, P.thr) ? k : 0.f, drop_keep16(h1, 1, P.thr) ? k : 0.f};
@@ -217,9 +217,9 @@ __device__ __forceinline__ void epilogue_store(const GemmParams& P, int gm, int 
 }
 
 namespace gpt2mi {
-extern bool g_gemm_persistent;  // gpt2mi_set_gemm_persistent
-// ring: the weight-gradient GEMMs (layout 2) on the 5-slot half-K-tile ring kernel
-int gemm256_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t s, int splits, bool ring = false);
-int gemm_pp_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t s, int splits, int map = 0);
+int gemm256_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t s, int splits);
+// persistent_ok: the caller allows the persistent (one block per CU) schedule (gpt2mi.h GPT2MI_SCHED_NO_PERSISTENT)
+int gemm_pp_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t s, int splits, int map = 0,
+                     bool persistent_ok = true);
 int splitk_reduce(const float* slab, int splits, size_t n, float* out, int accumulate, hipStream_t s);
 }

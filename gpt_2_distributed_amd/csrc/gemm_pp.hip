@@ -65,9 +65,13 @@ __device__ __forceinline__ int half_map(int ir, int h) {
 // One half-tile by LDS-DMA: 16 x 1 KiB instructions, 2 per wave.
 //   TRANS=0 (k-contiguous, src[row][k]): instruction covers image rows 8*ins..+8
 //   TRANS=1 (m-contiguous, src[k][row]): instruction covers k-rows 4*ins..+4
+//   rmax = the operand's last row (TRANS=0) / column (TRANS=1): a partial last tile reads clamped rows / columns
+// 16 zero bytes: the source of every lane of a zero K-tile's DMAs (gemm_pp_kernel, odd K-tile counts)
+__device__ const u32x4 g_zero16 = {0u, 0u, 0u, 0u};
+
 template <bool TRANS, bool IS_A, bool IL>
 __device__ __forceinline__ void dma_half(const bf16* __restrict__ src, int ld, int base, int h, int k0, int rmax,
-                                         char* slot, int wid, int lane) {
+                                         char* slot, int wid, int lane, bool zero = false) {
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     const int ins = wid * 2 + t;
@@ -79,7 +83,15 @@ __device__ __forceinline__ void dma_half(const bf16* __restrict__ src, int ld, i
     } else {
       const int k = 4 * ins + (lane >> 4);
       const int c = (lane & 15) ^ mc_swz(k);
+      // a partial last tile (extent % 256 != 0, a multiple of 64) reads past the row's end: the next row's elements,
+      // and past the operand's last row up to 192 elements (the caller's allocation covers them, gpt2mi.h); they
+      // only feed outputs the epilogue does not store
       g = src + (size_t)(k0 + k) * ld + base + half_map<IL, IS_A>(8 * c, h);
+    }
+    if (zero) {  // branch-free select of the zero source (zero is wave-uniform)
+      const uintptr_t zm = (uintptr_t)0 - (uintptr_t)zero;
+      g = reinterpret_cast<const bf16*>((reinterpret_cast<uintptr_t>(g) & ~zm) |
+                                        (reinterpret_cast<uintptr_t>(&g_zero16) & zm));
     }
     lds_dma16(g, slot + ins * 1024);
   }
@@ -236,7 +248,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wid >> 2, wc = wid & 3;
 
-  const int tiles_m = (P.M + BM - 1) / BM, tiles_n = P.N / BN;
+  // N (and, for the weight gradients, M) may end in a partial tile: a multiple of 64 (GPT-2 1.5B: 1600, 4800)
+  const int tiles_m = (P.M + BM - 1) / BM, tiles_n = (P.N + BN - 1) / BN;
   const int ntiles = tiles_m * tiles_n;
   // 1-D grid over (split, tile) items, split-major: the XCD remap gives each XCD a contiguous item range,
   // so the blocks of one K split (which share its A and B token rows) run out of one L2
@@ -247,7 +260,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   int m0, n0;
   tile_of(item - split * ntiles, tiles_m, tiles_n, m0, n0);
   const int kbeg = split * P.k_per_split;
-  const int nk = (min(P.K, kbeg + P.k_per_split) - kbeg) / BK;  // even (host-checked)
+  const int nk = (min(P.K, kbeg + P.k_per_split) - kbeg) / BK;  // even, or odd >= 3 without split-K (host-checked)
 
   // PERSIST: vector-memory stores each wave issues in an epilogue (one per output row and output array; the
   // column-sum atomic of waves 0-3 only makes the waits below retire more, never less)
@@ -268,7 +281,13 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   };
   zero_acc();
 
-  auto kofs = [&](int t) { return kbeg + t * BK; };
+  // An odd K-tile count (K = 1600 / 4800: GPT-2 1.5B; no split-K) runs as nk + 1 tiles whose tile 0 is a ZERO tile
+  // (both operands' LDS images zeroed, no DMA): the 4-phase pairs and their counted waits stay as they are (the
+  // waits for tile 0's missing DMAs are already satisfied), for one extra K-tile of MFMA work (1/26 at K = 1600).
+  const bool odd = !PERSIST && (nk & 1);
+  const int nkv = nk + (odd ? 1 : 0);  // virtual K-tile count, even
+  const int kbase = kbeg - (odd ? BK : 0);
+  auto kofs = [&](int t) { return kbase + t * BK; };
   // PERSIST (k-contiguous A and B): buffer DMA, 2 lane-offset VGPRs for every tile instead of per-tile
   // 64-bit row pointers (the persistent loop keeps its registers under the 256 of 2 waves/SIMD)
   [[maybe_unused]] u32x4 rs_a, rs_b;
@@ -293,14 +312,25 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   };
   auto dma_a = [&](int t, int h, char* buf) { dma_a_at(m0, t, h, buf); };
   auto dma_b = [&](int t, int h, char* buf) { dma_b_at(n0, t, h, buf); };
+  // tile 0 of the prologue (zero source when odd; the persistent kernel never is)
+  auto dma_a0z = [&](int t, int h, char* buf) {
+    if constexpr (PERSIST) dma_a_at(m0, t, h, buf);
+    else dma_half<A_T, true, AIL>(P.A, P.lda, m0, h, kofs(t), P.M - 1, buf + (h ? SA1 : SA0), wid, lane, odd);
+  };
+  auto dma_b0z = [&](int t, int h, char* buf) {
+    if constexpr (PERSIST) dma_b_at(n0, t, h, buf);
+    else dma_half<B_T, false, BIL>(P.B, P.ldb, n0, h, kofs(t), P.N - 1, buf + (h ? SB1 : SB0), wid, lane, odd);
+  };
   char* buf0 = smem;
   char* buf1 = smem + kBuf;
 
-  // prologue: what phases -6..-1 would have issued (all of tile 0, A_0 / B_0 of tile 1), in order
-  dma_a(0, 0, buf0);
-  dma_b(0, 0, buf0);
-  dma_b(0, 1, buf0);
-  dma_a(0, 1, buf0);
+  // prologue: what phases -6..-1 would have issued (all of tile 0, A_0 / B_0 of tile 1), in order. The zero tile
+  // of an odd count: the same DMAs with every lane's source redirected to 16 zero bytes (a select, no branch:
+  // a branch here costs the main loop registers)
+  dma_a0z(0, 0, buf0);
+  dma_b0z(0, 0, buf0);
+  dma_b0z(0, 1, buf0);
+  dma_a0z(0, 1, buf0);
   dma_a(1, 0, buf1);
   dma_b(1, 0, buf1);
   asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A_0(0), B_0(0) landed
@@ -311,54 +341,55 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   for (;;) {  // PERSIST: one iteration per output tile (non-persistent: exactly one)
 
   Frags fr;
-  // One K-tile (4 phases) of the pair starting at t: S = 0 / 1 is the tile's parity. In the last pair
-  // (LAST) the DMAs for tiles >= nk are not issued, and each wait retires what the next phase reads
-  // from the real DMAs still outstanding (vmcnt 8,8,6,4 | 2,0,0,0 instead of 8 everywhere): no re-load
-  // traffic, and nothing left in flight for the epilogue to wait for.
+  // One K-tile (4 phases): tile tt = t + S, S = 0 / 1 its buffer parity. HN / HN2: tiles tt + 1 / tt + 2 exist. The
+  // DMAs for tiles past the end are not issued, and each wait retires what the next phase reads from the real DMAs
+  // still outstanding: vmcnt 8,8,8,8 (steady state), 8,8,6,4 (the second-to-last tile), 2,0,0,0 (the last): no
+  // re-load traffic, and nothing left in flight for the epilogue to wait for. The counts depend only on (HN, HN2), so
+  // an odd number of K-tiles ends ..., (T,T) at parity 0, (T,F) at parity 1, (F,F) at parity 0 (K = 1600 / 4800:
+  // GPT-2 1.5B).
   //
   // FIRST (persistent schedule, K-tile 0 of a tile after an epilogue): the waits of phases 1-2 retire half-tiles
   // issued BEFORE the previous tile's epilogue stores. vmcnt counts loads, stores and LDS-DMA together in issue
   // order and waits for all but the N youngest, so those waits count the epilogue's kStores stores among the
   // younger operations instead of draining them: the stores get two more phases to complete in the background.
-  auto ktile = [&](int t, auto s_c, auto last_c) {
+  auto ktile = [&](int t, auto s_c, auto hn_c, auto hn2_c) {
     constexpr int S = decltype(s_c)::value;
-    constexpr bool LAST = decltype(last_c)::value;
+    constexpr bool HN = decltype(hn_c)::value;    // tile tt + 1 exists
+    constexpr bool HN2 = decltype(hn2_c)::value;  // tile tt + 2 exists
     // PERSIST, K-tile 0 (t == 0, S == 0) of a tile that follows an epilogue: phases 1-2 wait with the epilogue's
-    // stores counted as younger (a wave-uniform branch around the wait alone; nk >= 4 host-checked, so K-tile 0
-    // is never in the LAST pair)
-    const bool first = PERSIST && S == 0 && !LAST && t == 0 && after_epi;
-    constexpr bool next_dma = !LAST || S == 0;  // tile tt + 1 exists
-    constexpr bool next2_dma = !LAST;           // tile tt + 2 exists
+    // stores counted as younger (a wave-uniform branch around the wait alone; nk >= 4 and even, host-checked, so
+    // K-tile 0 is always a steady-state tile)
+    const bool first = PERSIST && S == 0 && HN2 && t == 0 && after_epi;
     char* cur = S ? buf1 : buf0;
     char* nxt = S ? buf0 : buf1;
     const int tt = t + S;
     // phase 1: quadrant (0,0)
     read_a<A_T>(fr, cur + SA0, wr, lane);
     read_b<B_T, 0>(fr, cur + SB0, wc, lane);
-    if constexpr (next_dma) dma_b(tt + 1, 1, nxt);
-    PP_SYNC_MFMA_F(acc[0][0], 0, (!LAST || S == 0) ? 8 : 2, first)
+    if constexpr (HN) dma_b(tt + 1, 1, nxt);
+    PP_SYNC_MFMA_F(acc[0][0], 0, HN ? 8 : 2, first)
     // phase 2: quadrant (0,1)
     read_b<B_T, 1>(fr, cur + SB1, wc, lane);
-    if constexpr (next_dma) dma_a(tt + 1, 1, nxt);
-    PP_SYNC_MFMA_F(acc[0][1], 1, (!LAST || S == 0) ? 8 : 0, first)
+    if constexpr (HN) dma_a(tt + 1, 1, nxt);
+    PP_SYNC_MFMA_F(acc[0][1], 1, HN ? 8 : 0, first)
     // phase 3: quadrant (1,1)
     read_a<A_T>(fr, cur + SA1, wr, lane);
-    if constexpr (next2_dma) dma_a(tt + 2, 0, cur);
-    PP_SYNC_MFMA(acc[1][1], 1, !LAST ? 8 : (S == 0 ? 6 : 0))
+    if constexpr (HN2) dma_a(tt + 2, 0, cur);
+    PP_SYNC_MFMA(acc[1][1], 1, HN2 ? 8 : (HN ? 6 : 0))
     // phase 4: quadrant (1,0) from registers
-    if constexpr (next2_dma) dma_b(tt + 2, 0, cur);
-    PP_SYNC_MFMA(acc[1][0], 0, !LAST ? 8 : (S == 0 ? 4 : 0))
+    if constexpr (HN2) dma_b(tt + 2, 0, cur);
+    PP_SYNC_MFMA(acc[1][0], 0, HN2 ? 8 : (HN ? 4 : 0))
   };
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
   using F = std::false_type;
   using Tr = std::true_type;
-  for (int t = 0; t < nk - 2; t += 2) {
-    ktile(t, I0{}, F{});
-    ktile(t, I1{}, F{});
+  for (int t = 0; t < nkv - 2; t += 2) {
+    ktile(t, I0{}, Tr{}, Tr{});
+    ktile(t, I1{}, Tr{}, Tr{});
   }
-  ktile(nk - 2, I0{}, Tr{});
-  ktile(nk - 2, I1{}, Tr{});
+  ktile(nkv - 2, I0{}, Tr{}, F{});
+  ktile(nkv - 2, I1{}, F{}, F{});
   if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the groups (same barrier count)
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
@@ -379,7 +410,10 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   // (one 16-B store per row pair and output array); otherwise columns 4ch..4ch+3 of one row
   const int cj = tid & 31, hl = (tid >> 5) & 1;
   const int gnb = kWide ? n0 + 8 * cj : gn;  // first bias column of the lane
-  const bool has_bias = P.bias && EPI != EPI_GELU_BWD;
+  // lanes whose columns lie past N (a partial last column tile; N % 64 == 0, so a lane's 4 / 8 columns are all in or
+  // all out) load no operands and store nothing
+  const bool col_ok = PERSIST || gnb < P.N;  // (the persistent schedule runs full column tiles only)
+  const bool has_bias = P.bias && EPI != EPI_GELU_BWD && col_ok;
   const f32x4 bias = has_bias ? *reinterpret_cast<const f32x4*>(P.bias + gnb) : f32x4{0.f, 0.f, 0.f, 0.f};
   [[maybe_unused]] f32x4 bias1 = {0.f, 0.f, 0.f, 0.f};
   if constexpr (kWide) {
@@ -550,7 +584,7 @@ write_image(mi, 0);
   } else if constexpr (kWide) {
     // one-tile-per-block, bf16 outputs: two 128-row passes; wave wid, half hl takes rows 16it + 2wid + hl
     // (it = 0..7) of the pass, columns 8cj..8cj+7, one 16-B store per row pair and output array
-    const bool full = m0 + BM <= P.M;  // block-uniform
+    const bool full = m0 + BM <= P.M && n0 + BN <= P.N;  // block-uniform
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi) {
       [[maybe_unused]] bf16x8 op8[8];
@@ -559,7 +593,7 @@ write_image(mi, 0);
         for (int it = 0; it < 8; ++it)
           op8[it] = *reinterpret_cast<const bf16x8*>(
               reinterpret_cast<const bf16*>(P.aux) +
-              (size_t)min(m0 + mi * 128 + 16 * it + 2 * wid + hl, P.M - 1) * P.ldaux + gnb);
+              (size_t)min(m0 + mi * 128 + 16 * it + 2 * wid + hl, P.M - 1) * P.ldaux + min(gnb, P.N - 8));
       }
       if (mi) lds_barrier();  // pass 0's reads are done before pass 1 overwrites the image
 write_image(mi, wr * 64);
@@ -582,7 +616,7 @@ write_image(mi, wr * 64);
         for (int k = 0; k < 4; ++k) {
           const int it = 4 * half + k;
           const int gm = m0 + mi * 128 + 16 * it + 2 * wid + hl;
-          if (GUARD && gm >= P.M) continue;
+          if (GUARD && (gm >= P.M || !col_ok)) continue;
           f32x4 w0 = va[k], w1 = vb[k];
           w0 += bias;  // vector adds: packed without SLP
           w1 += bias1;
@@ -617,7 +651,7 @@ write_image(mi, wr * 64);
       for (int it = 0; it < 16; ++it) {
         const int r = it * 8 + wid;
         const int gm = m0 + (AIL ? ((r >> 6) << 7) + mi * 64 + (r & 63) : mi * 128 + r);
-        opnd[it] = epilogue_operand<EPI>(P, min(gm, P.M - 1), gn);
+        opnd[it] = epilogue_operand<EPI>(P, min(gm, P.M - 1), min(gn, P.N - 4));
       }
     }
     if (mi) lds_barrier();  // pass 0's reads are done before pass 1 overwrites the image
@@ -644,7 +678,7 @@ write_image(mi, wr * 64);
         }
       }
     };
-    if (m0 + BM <= P.M) {  // full tile (block-uniform): straight-line reads, then the stores
+    if (m0 + BM <= P.M && n0 + BN <= P.N) {  // full tile (block-uniform): straight-line reads, then the stores
       f32x4 v[16];
 #pragma unroll
       for (int it = 0; it < 16; ++it) {
@@ -662,7 +696,7 @@ write_image(mi, wr * 64);
       for (int it = 0; it < 16; ++it) {
         const int r = it * 8 + wid;
         const f32x4 v = *reinterpret_cast<const f32x4*>(img + r * 256 + 4 * (ch ^ (r & 15)));
-        if (row_of(it) < P.M) finish(it, v, std::integral_constant<int, -1>{});
+        if (row_of(it) < P.M && col_ok) finish(it, v, std::integral_constant<int, -1>{});
       }
     }
   }
@@ -684,7 +718,7 @@ write_image(mi, wr * 64);
         *reinterpret_cast<f32x4*>(img + (tid >> 6) * 256 + 4 * ch) = csum;
       }
       lds_barrier();
-      if (tid < 256) {
+      if (tid < 256 && n0 + tid < P.N) {
         float t = 0.f;
 #pragma unroll
         for (int w8 = 0; w8 < 8; ++w8) t += img[w8 * 256 + tid];
@@ -722,7 +756,7 @@ write_image(mi, wr * 64);
 // k-contiguous forward operands).
 template <bool A_T, bool B_T, int EPI, int MAP = (A_T ? 1 : 0) | (B_T ? 2 : 0)>
 int launch(const GemmParams& P, hipStream_t s, int splits) {
-  dim3 grid(((P.M + BM - 1) / BM) * (P.N / BN) * splits);
+  dim3 grid(((P.M + BM - 1) / BM) * ((P.N + BN - 1) / BN) * splits);
   gemm_pp_kernel<A_T, B_T, EPI, MAP><<<grid, kThreads, 0, s>>>(P);
   return gpt2mi::check_launch("gemm_pp");
 }
@@ -742,7 +776,7 @@ int num_cus() {
 // persistent variant: one block per CU, grid a multiple of 8
 template <int EPI>
 int launch_persistent(const GemmParams& P, hipStream_t s) {
-  const int ntiles = ((P.M + BM - 1) / BM) * (P.N / BN);
+  const int ntiles = ((P.M + BM - 1) / BM) * (P.N / BN);  // N % 256 == 0 (gemm_pp_dispatch)
   dim3 grid(min(ntiles, num_cus()));
   gemm_pp_kernel<false, false, EPI, 0, true><<<grid, kThreads, 0, s>>>(P);
   return gpt2mi::check_launch("gemm_pp_persistent");
@@ -758,8 +792,13 @@ namespace gpt2mi {
 constexpr int g_persist_kmax = GPT2MI_PERSIST_KMAX;
 // Layouts 0 / 1; N % 256 == 0, every split's K range an even number (>= 2) of 64-deep tiles.
 // Returns -1 when this kernel does not apply (the caller falls back).
-int gemm_pp_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t s, int splits, int map) {
-  if (P.N % BN != 0 || P.k_per_split % (2 * BK) != 0 || P.K % (2 * BK) != 0) return -1;
+int gemm_pp_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t s, int splits, int map,
+                     bool persistent_ok) {
+  // N (and M) multiples of 64; without split-K any K-tile count >= 2 (an odd count ends in a single K-tile); with
+  // split-K an even count per split
+  if (P.N % 64 != 0 || P.M % 64 != 0 || P.K % BK != 0 || P.K < 2 * BK) return -1;
+  if (splits > 1 && (P.k_per_split % (2 * BK) != 0 || P.K % (2 * BK) != 0)) return -1;
+  if (splits == 1 && P.k_per_split != P.K) return -1;
   // wgrad (both operands m-contiguous): this kernel since the LDS-DMA went to inline asm (lm_head wgrad 4046 vs
   // 4485 us on the 2-stage gemm256 kernel, qkv 197 vs 230; before, hipcc's vmcnt(0) drains made it the slower
   // one, 698-721 vs 765 TF). map 8 = the same (tools/lib_ab.py impl 8)
@@ -768,7 +807,7 @@ int gemm_pp_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t 
     return epilogue == EPI_SLAB ? launch<true, true, EPI_SLAB>(P, s, splits)
                                 : epilogue == EPI_F32 ? launch<true, true, EPI_F32>(P, s, 1) : -1;
   }
-  if (map > 0 && epilogue == EPI_BF16 && layout <= 1) {  // half-tile map experiments (tools/gemm_probe.py)
+  if (map > 0 && epilogue == EPI_BF16 && layout <= 1 && P.N % BN == 0) {  // half-tile maps (tools/gemm_probe.py)
     if (layout == 0) {
       if (map == 1) return launch<false, false, EPI_BF16, 1>(P, s, 1);
       if (map == 2) return launch<false, false, EPI_BF16, 2>(P, s, 1);
@@ -783,8 +822,11 @@ int gemm_pp_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t 
   // the persistent one at any K: tools/gemm_ab.py). Epilogue operand loads (residual, GELU derivative) are
   // issued after the next tile's asm DMAs, so the compiler's wait for them retires those DMAs too — early,
   // never late.
-  const int ntiles = ((P.M + BM - 1) / BM) * (P.N / BN);
-  if (layout == 0 && (map == 7 || (map == 0 && g_gemm_persistent && P.K <= g_persist_kmax)) && P.K >= 4 * BK &&
+  const int ntiles = ((P.M + BM - 1) / BM) * ((P.N + BN - 1) / BN);
+  // (full column tiles and an even K-tile count only: the persistent epilogue has no column guard, and its K-tile 0
+  // must be a steady-state tile)
+  if (layout == 0 && (map == 7 || (map == 0 && persistent_ok && P.K <= g_persist_kmax)) && P.K >= 4 * BK &&
+      P.N % BN == 0 && P.K % (2 * BK) == 0 &&
       ntiles >= 2 * num_cus() &&
       ((epilogue == EPI_BF16 && P.dbias == nullptr) || epilogue == EPI_GELU || epilogue == EPI_RESID ||
        epilogue == EPI_GELU_BWD) &&

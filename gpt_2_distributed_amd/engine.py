@@ -32,6 +32,7 @@ HBM layout per (B, T) workspace (M = B*T tokens, C = n_embd, Vp = vocab padded t
 """
 from __future__ import annotations
 
+import weakref
 from dataclasses import dataclass
 from typing import Dict, List, Optional
 
@@ -40,6 +41,7 @@ import torch.nn.functional as F
 
 from . import _lib as K
 from ._lib import wgrad_splits as K_wgrad_splits
+from .dropout_keys import MULTIPLIERS
 
 BF16 = torch.bfloat16
 F32 = torch.float32
@@ -53,6 +55,53 @@ def _mix(*xs: int) -> int:
         h ^= (x + 0x9E3779B97F4A7C15 + ((h << 6) & 0xFFFFFFFFFFFFFFFF) + (h >> 2)) & 0xFFFFFFFFFFFFFFFF
         h = (h * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
     return h
+
+
+def site_seeds(base_seed: int, step_seed: int, n_layer: int) -> dict:
+    """The 64-bit dropout seed of every site of one step ("embd", ("attn"|"proj"|"fc1"|"fc2", l)): the low word a
+    mixed counter offset, the high word the site's vetted second-round multiplier (dropout_keys.py; site i takes
+    entry i, so no two sites of a step share one: their masks are distinct functions, csrc/common.h)."""
+    def seed(i, *key):
+        return (MULTIPLIERS[i % len(MULTIPLIERS)] << 32) | (_mix(base_seed, step_seed, *key) & 0xFFFFFFFF)
+    s = {"embd": seed(0, 0xE)}
+    for l in range(n_layer):
+        for k, site in enumerate(("attn", "proj", "fc1", "fc2")):
+            s[(site, l)] = seed(1 + 4 * l + k, l, k + 1)
+    return s
+
+
+# Activation buffers carry this many elements of slack past their end: the weight-gradient GEMM of a width that is not
+# a multiple of 256 (GPT-2 1.5B: 1600, 4800) reads its partial last tile's columns up to 192 elements past the
+# operand's last row (gpt2mi.h gpt2mi_gemm_wgrad)
+ACT_TAIL = 256
+
+
+def act_empty(*shape, dtype, device):
+    n = 1
+    for d in shape:
+        n *= d
+    return torch.empty(n + ACT_TAIL, dtype=dtype, device=device)[:n].view(*shape)
+
+
+def watch_optimizer_steps(owner, params, on_step) -> None:
+    """Call on_step(owner) after any torch optimizer step that updates one of `params` (a global post-step hook).
+    In-place updates normally bump a tensor's version counter, which is how the engine notices that its bf16
+    shadow (or an FSDP wrapper that its gathered units) went stale, but torch's fused AdamW kernel
+    (torch.optim.AdamW(fused=True), the reference trainer's optimizer, train_gpt2_distributed.py:356-362) does not
+    bump it. The repo's own optimizers (``_gpt2mi_fused``) refresh the copies themselves and are skipped."""
+    ids = {id(p) for p in params}
+    ref = weakref.ref(owner)
+
+    def hook(opt, args, kwargs):
+        o = ref()
+        if o is None or getattr(opt, "_gpt2mi_fused", False):
+            return
+        if any(id(p) in ids for g in opt.param_groups for p in g["params"]):
+            on_step(o)
+
+    from torch.optim.optimizer import register_optimizer_step_post_hook
+    handle = register_optimizer_step_post_hook(hook)
+    weakref.finalize(owner, handle.remove)
 
 
 def padded_len(T: int) -> int:
@@ -77,7 +126,7 @@ class BlockActs:
     @staticmethod
     def alloc(cfg, B, T, device, act, xmid=True):
         M, C, H = B * T, cfg.n_embd, cfg.n_head
-        e = lambda *s, dt=act: torch.empty(*s, dtype=dt, device=device)  # noqa: E731
+        e = lambda *s, dt=act: act_empty(*s, dtype=dt, device=device)  # noqa: E731
         return BlockActs(ln1=e(M, C), m1=e(M, dt=F32), r1=e(M, dt=F32), qkv=e(M, 3 * C), ao=e(M, C),
                          lse=e(B * H, T, dt=F32), xmid=e(M, C, dt=F32) if xmid else None, ln2=e(M, C),
                          m2=e(M, dt=F32), r2=e(M, dt=F32), dgelu=e(M, 4 * C), h=e(M, 4 * C))
@@ -89,7 +138,7 @@ class Scratch:
     def __init__(self, cfg, B, T, vpad, device, act, head=True):
         C, H = cfg.n_embd, cfg.n_head
         M = B * T
-        e = lambda *s, dt=act: torch.empty(*s, dtype=dt, device=device)  # noqa: E731
+        e = lambda *s, dt=act: act_empty(*s, dtype=dt, device=device)  # noqa: E731
         self.dres = e(M, C, dt=F32)
         self.dres_bf = e(M, C)
         self.dln = e(M, C)
@@ -101,7 +150,7 @@ class Scratch:
         # split-K slabs of the 256x256 wgrad GEMMs
         wshapes = [(3 * C, C), (C, C), (4 * C, C), (C, 4 * C)] + ([(vpad, C)] if head else [])
         need = max((K_wgrad_splits(m, n, M) * m * n if K_wgrad_splits(m, n, M) > 1 else 0)
-                   for m, n in wshapes) if C % 256 == 0 and act == BF16 else 0
+                   for m, n in wshapes) if C % 64 == 0 and act == BF16 else 0
         self.wgrad_ws = e(max(need, 4), dt=F32)
 
 
@@ -110,7 +159,7 @@ class Workspace(Scratch):
         super().__init__(cfg, B, T, vpad, device, act, head=True)
         L, C = cfg.n_layer, cfg.n_embd
         M = B * T
-        e = lambda *s, dt=act: torch.empty(*s, dtype=dt, device=device)  # noqa: E731
+        e = lambda *s, dt=act: act_empty(*s, dtype=dt, device=device)  # noqa: E731
         self.act = act
         self.B, self.T, self.M = B, T, M
         self.x = e(L + 1, M, C, dt=F32)
@@ -238,6 +287,11 @@ class GradHooks:
     def end_backward(self) -> None:
         """The backward's last kernel is enqueued: finish the collective before backward returns."""
 
+    def backward_sched(self, base: int) -> int:
+        """The GEMM schedule flags of this backward's launches (_lib.SCHED_*): a wrapper whose collectives run
+        concurrently with the backward keeps the persistent schedule off."""
+        return base
+
     def fwd_unit(self, unit: str) -> None:
         """FSDP: the parameters of ``unit`` ("embed", "h.<l>", "head") are about to be read."""
 
@@ -279,10 +333,15 @@ class Engine:
         self._params = list(model.parameters())
         self.params_by_name = dict(model.named_parameters())
         self.probes: Dict[str, list] = {}  # name -> [(start_event, end_event)] recorded when armed
+        # GEMM schedule flags passed with every launch (gpt2mi.h GPT2MI_SCHED_*): base_sched for this engine (FSDP,
+        # whose collectives overlap every pass, sets NO_PERSISTENT), gemm_sched for the running pass
+        self.base_sched = K.SCHED_AUTO
+        self.gemm_sched = K.SCHED_AUTO
         if not hasattr(K, "load") or self.device.type != "cuda":
             raise RuntimeError("the engine needs the model on a cuda (MI355X) device")
         K.load()
         self.refresh_shadow()
+        watch_optimizer_steps(self, self._params, Engine.mark_shadow_stale)
 
     # ---- live per-kernel timing (bench.py): HIP events on the launch stream around named launches ----
     def _probe(self, name):
@@ -290,6 +349,12 @@ class Engine:
         if lst is None:
             return _NullCtx
         return _EventCtx(lst)
+
+    def _gemm(self, *a, **kw):
+        K.gemm(*a, sched=self.gemm_sched, **kw)
+
+    def _gemm_wgrad(self, *a, **kw):
+        K.gemm_wgrad(*a, sched=self.gemm_sched, **kw)
 
     # ---- parameter views ------------------------------------------------------------------------------
     def p(self, name):  # fp32 master view
@@ -311,6 +376,11 @@ class Engine:
 
     def _versions(self):
         return tuple(p._version for p in self._params)
+
+    def mark_shadow_stale(self):
+        """A foreign in-place update of the master weights: re-cast the shadows before the next forward."""
+        self._shadow_versions = None
+        self._shadowT_stale = True
 
     def mark_shadow_fresh(self):
         self._shadow_versions = self._versions()
@@ -374,9 +444,9 @@ class Engine:
 
     def _lazy_zero_ok(self, act):
         # every weight-gradient GEMM of the full backward takes a path with a write-or-accumulate choice
-        # (gemm_wgrad / EPI_F32; not the EPI_ATOMIC fallback of widths that are not multiples of 256), and
+        # (gemm_wgrad / EPI_F32; not the EPI_ATOMIC fallback of widths that are not multiples of 64), and
         # the arena is the engine's own (FSDP zeroes per unit)
-        return act == BF16 and self.param_provider is None and self.cfg.n_embd % 256 == 0
+        return act == BF16 and self.param_provider is None and self.cfg.n_embd % 64 == 0
 
     def _zero_accumulated(self):
         """Zero the arena outside the GEMM-written weight slots (wte with its pad rows, the four matrices of
@@ -420,6 +490,8 @@ class Engine:
         self._prepare_grads(act if full else None)
         self.bwd_act = act  # the precision of this backward's gradients (FSDP reduces in it)
         scale = self.grad_sync.begin_backward() if self.grad_sync is not None else 1.0
+        self.gemm_sched = self.grad_sync.backward_sched(self.base_sched) if self.grad_sync is not None \
+            else self.base_sched
         self.grad_dirty = True
         return scale
 
@@ -429,6 +501,7 @@ class Engine:
 
     def _end_grads(self):
         self._grad_fresh = False
+        self.gemm_sched = self.base_sched
         if self.grad_sync is not None:
             self.grad_sync.end_backward()
 
@@ -497,12 +570,7 @@ class Engine:
         return float(self.cfg.resid_pdrop), float(self.cfg.attn_pdrop)
 
     def _seeds(self, step_seed):
-        L = self.cfg.n_layer
-        s = {"embd": _mix(self.base_seed, step_seed, 0xE)}
-        for l in range(L):
-            for k, site in enumerate(("attn", "proj", "fc1", "fc2")):
-                s[(site, l)] = _mix(self.base_seed, step_seed, l, k + 1)
-        return s
+        return site_seeds(self.base_seed, step_seed, self.cfg.n_layer)
 
     def _next_seeds(self):
         self._step_seed += 1
@@ -521,11 +589,11 @@ class Engine:
         C, H = self.cfg.n_embd, self.cfg.n_head
         M = B * T
         pre = f"transformer.h.{l}."
-        K.gemm(K.FWD, K.EPI_BF16, M, 3 * C, C, A.ln1, C, self.w(pre + "attn.qkv.weight", act), C, A.qkv, 3 * C,
+        self._gemm(K.FWD, K.EPI_BF16, M, 3 * C, C, A.ln1, C, self.w(pre + "attn.qkv.weight", act), C, A.qkv, 3 * C,
                bias=self.p(pre + "attn.qkv.bias"))
         with self._probe("attn_fwd"):
             K.attn_fwd(A.qkv, A.ao, A.lse, B, T, H, C // H, pa, seeds[("attn", l)])
-        K.gemm(K.FWD, K.EPI_RESID, M, C, C, A.ao, C, self.w(pre + "attn.proj.weight", act), C, out, C,
+        self._gemm(K.FWD, K.EPI_RESID, M, C, C, A.ao, C, self.w(pre + "attn.proj.weight", act), C, out, C,
                bias=self.p(pre + "attn.proj.bias"), resid=resid, p_drop=pr, seed=seeds[("proj", l)])
 
     def _mlp_fwd(self, l, A, resid, out, M, act, pr, seeds):
@@ -533,9 +601,9 @@ class Engine:
         C = self.cfg.n_embd
         pre = f"transformer.h.{l}."
         with self._probe("fc1_fwd"):
-            K.gemm(K.FWD, K.EPI_GELU, M, 4 * C, C, A.ln2, C, self.w(pre + "mlp.fc1.weight", act), C, A.h, 4 * C,
+            self._gemm(K.FWD, K.EPI_GELU, M, 4 * C, C, A.ln2, C, self.w(pre + "mlp.fc1.weight", act), C, A.h, 4 * C,
                    bias=self.p(pre + "mlp.fc1.bias"), aux=A.dgelu, ldaux=4 * C, p_drop=pr, seed=seeds[("fc1", l)])
-        K.gemm(K.FWD, K.EPI_RESID, M, C, 4 * C, A.h, 4 * C, self.w(pre + "mlp.fc2.weight", act), 4 * C, out, C,
+        self._gemm(K.FWD, K.EPI_RESID, M, C, 4 * C, A.h, 4 * C, self.w(pre + "mlp.fc2.weight", act), 4 * C, out, C,
                bias=self.p(pre + "mlp.fc2.bias"), resid=resid, p_drop=pr, seed=seeds[("fc2", l)])
 
     def _block_fwd(self, l, A, x_in, x_out, B, T, act, pr, pa, seeds):
@@ -568,23 +636,23 @@ class Engine:
 
     def _wgrad_launch(self, S, act, m, n, M, a, lda, b, ldb, out):
         if act == F32:
-            K.gemm(K.WGRAD, K.EPI_F32, m, n, M, a, lda, b, ldb, out, n, accumulate=not self._grad_fresh)
-        elif m % 256 == 0 and n % 256 == 0:
-            K.gemm_wgrad(m, n, M, a, lda, b, ldb, out, n, accumulate=not self._grad_fresh, workspace=S.wgrad_ws,
+            self._gemm(K.WGRAD, K.EPI_F32, m, n, M, a, lda, b, ldb, out, n, accumulate=not self._grad_fresh)
+        elif m % 64 == 0 and n % 64 == 0:  # (1.5B: a partial 64-multiple last tile, 1600 / 4800)
+            self._gemm_wgrad(m, n, M, a, lda, b, ldb, out, n, accumulate=not self._grad_fresh, workspace=S.wgrad_ws,
                          splits=K_wgrad_splits(m, n, M))
         else:
             assert not self._grad_fresh, "atomic weight gradients need a zeroed arena"
             s = self.WGRAD_SPLITS
             while s > 1 and M % (64 * s) != 0:
                 s //= 2
-            K.gemm(K.WGRAD, K.EPI_ATOMIC, m, n, M, a, lda, b, ldb, out, n, splits=s)
+            self._gemm(K.WGRAD, K.EPI_ATOMIC, m, n, M, a, lda, b, ldb, out, n, splits=s)
 
     def _dgrad(self, act, M, out, dy, wname, n_in, n_out, epi=K.EPI_BF16, **kw):
         # dX[M][n_in] = dY[M][n_out] . W[n_out][n_in]: the forward layout against W^T when it exists
         if act == BF16 and self.wT_ok(wname):
-            K.gemm(K.FWD, epi, M, n_in, n_out, dy, n_out, self.wT16(wname), n_out, out, n_in, **kw)
+            self._gemm(K.FWD, epi, M, n_in, n_out, dy, n_out, self.wT16(wname), n_out, out, n_in, **kw)
         else:
-            K.gemm(K.DGRAD, epi, M, n_in, n_out, dy, n_out, self.w(wname, act), n_in, out, n_in, **kw)
+            self._gemm(K.DGRAD, epi, M, n_in, n_out, dy, n_out, self.w(wname, act), n_in, out, n_in, **kw)
 
     def _mlp_bwd(self, l, A, S, dY, dx_out, M, act):
         """dY = grad of the fc2 output with drop2 applied (its bias grad already taken) -> dx_out = grad of
@@ -671,6 +739,7 @@ class Engine:
 
     def _forward(self, idx, labels, need_grad):
         cfg = self.cfg
+        self.gemm_sched = self.base_sched  # (a backward that raised midway left its flags)
         V, Vp, C = cfg.vocab_size, self.vpad, cfg.n_embd
         idx, labels, T = self._pad(idx, labels)
         B, Tp = idx.shape
@@ -685,13 +754,16 @@ class Engine:
         self._trunk_fwd(ws, idx, B, Tp, T, act, pr, pa, seeds)
         logits = torch.empty(M, Vp, dtype=act, device=self.device)  # fresh: the caller may keep it
         with self._probe("lm_head_fwd"):
-            K.gemm(K.FWD, K.EPI_BF16, M, Vp, C, ws.lnf, C, self.w("transformer.wte.weight", act), C, logits, Vp)
+            self._gemm(K.FWD, K.EPI_BF16, M, Vp, C, ws.lnf, C, self.w("transformer.wte.weight", act), C, logits, Vp)
         loss = None
         if labels is not None:
             loss = torch.empty((), dtype=F32, device=self.device)  # fresh: callers may keep it across steps
             K.xent_fwd(logits, Vp, labels, ws.loss_rows, ws.lse_ce, ws.dlogits if need_grad else None, Vp, M, V,
                        loss, ws.inv_count)
-        return logits.view(B, Tp, Vp)[:, :T, :V], loss
+        out = logits.view(B, Tp, Vp)
+        if Tp != T:  # compact rows, so the reference's own logits.view(-1, V) (model.py:357-358) merges B and T
+            out = out[:, :T].contiguous()
+        return out[..., :V], loss
 
     def _backward(self, grad_logits, grad_loss):
         cfg = self.cfg
@@ -720,17 +792,18 @@ class Engine:
                         alpha=gs)
         wte_g = self.layout.padded_view(self.grad, "transformer.wte.weight", Vp)
         with self._probe("lm_head_wgrad"), self._probe("wgrad"):
-            if C % 256 == 0 and act == BF16:
-                K.gemm_wgrad(Vp, C, M, ws.dlogits, Vp, ws.lnf, C, wte_g, C, accumulate=not self._grad_fresh,
+            if C % 64 == 0 and act == BF16:
+                self._gemm_wgrad(Vp, C, M, ws.dlogits, Vp, ws.lnf, C, wte_g, C, accumulate=not self._grad_fresh,
                              alpha_dev=alpha_dev, alpha=gs, workspace=ws.wgrad_ws, splits=K_wgrad_splits(Vp, C, M))
             else:
-                K.gemm(K.WGRAD, K.EPI_F32, Vp, C, M, ws.dlogits, Vp, ws.lnf, C, wte_g, C, alpha_dev=alpha_dev,
+                self._gemm(K.WGRAD, K.EPI_F32, Vp, C, M, ws.dlogits, Vp, ws.lnf, C, wte_g, C, alpha_dev=alpha_dev,
                        alpha=gs, accumulate=not self._grad_fresh)
         self._trunk_bwd(ws, sv)
         self._end_grads()
 
     # ---- GPT2Backbone.forward on its own -------------------------------------------------------------
     def _trunk_forward_module(self, idx, need_grad):
+        self.gemm_sched = self.base_sched  # (a backward that raised midway left its flags)
         idx, _, T = self._pad(idx, None)
         B, Tp = idx.shape
         act = self.compute_dtype()
@@ -765,6 +838,7 @@ class Engine:
     def _sub_forward(self, kind, l, x, need_grad):
         """kind: "block" (x = residual stream, model.py:213-219), "mlp" (x = ln2 output, model.py:186-192),
         "attn" (x = ln1 output, model.py:110-159). Returns (y, saved state)."""
+        self.gemm_sched = self.base_sched  # (a backward that raised midway left its flags)
         cfg = self.cfg
         C = cfg.n_embd
         if x.dim() != 3 or x.shape[-1] != C:
@@ -810,7 +884,7 @@ class Engine:
     def _to_act(xf, act):
         if act == F32:
             return xf
-        out = torch.empty(xf.shape, dtype=BF16, device=xf.device)
+        out = act_empty(*xf.shape, dtype=BF16, device=xf.device)  # (a weight-gradient operand: tail slack)
         K.cast_f32_bf16(xf, out, xf.numel())
         return out
 

@@ -21,6 +21,8 @@ from . import _lib as K
 
 
 class _FlatAdamW(torch.optim.Optimizer):
+    _gpt2mi_fused = True  # refreshes the engine's shadows itself (engine.watch_optimizer_steps skips it)
+
     def __init__(self, params, p_flat, lr, betas, eps, weight_decay):
         super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay))
         n = p_flat.numel()
@@ -97,6 +99,8 @@ class ShardedAdamW(_FlatAdamW):
             with torch.enable_grad():
                 loss = closure()
         f = self.fsdp
+        if f.flat_param.grad is None:
+            return loss  # no backward since zero_grad(set_to_none=True): skipped, as torch's optimizers do
         self._run(f.flat_param.detach(), f.grad_shard, f.shard_bf16)
         f.mark_params_updated(bf16_fresh=True)
         if f.coll:  # the clip_grad_norm_(inf) value of the full model: sum of squares over shards

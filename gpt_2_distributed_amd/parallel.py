@@ -187,11 +187,18 @@ class _DDPHooks(_DPHooks):
 
     def begin_backward(self) -> float:
         if self.sync and self.coll:
-            # the buckets' RCCL kernels run under the rest of the backward: no persistent GEMM grid there
-            # (a block waiting for a CU held by a collective would hold the whole grid back; gpt2mi.h)
-            from . import _lib as K
-            K.set_gemm_persistent(False)
+            # a backward that raised midway left buckets in flight and `next` past them: wait for those (their
+            # spans are re-reduced by this backward anyway) and start over
+            for w in self.reducer.works:
+                w.wait()
+            self.reducer.reset()
         return super().begin_backward()
+
+    def backward_sched(self, base: int) -> int:
+        # the buckets' RCCL kernels run under the rest of the backward: no persistent GEMM grid there (a block
+        # waiting for a CU held by a collective would hold the whole grid back; gpt2mi.h GPT2MI_SCHED_NO_PERSISTENT)
+        from . import _lib as K
+        return base | K.SCHED_NO_PERSISTENT if self.sync and self.coll else base
 
     def ready(self, name):
         if self.sync and self.coll:
@@ -200,8 +207,6 @@ class _DDPHooks(_DPHooks):
     def end_backward(self):
         if self.sync and self.coll:
             self.reducer.finish()
-            from . import _lib as K
-            K.set_gemm_persistent(True)
 
 
 class DistributedDataParallel(nn.Module):
@@ -304,9 +309,9 @@ class FullyShardedDataParallel(nn.Module):
         if self.coll:
             dist.broadcast(module.arena, src=0)
             # prefetched all-gathers and reduce-scatters overlap the forward and the backward: no persistent
-            # GEMM grids in this process (see _DDPHooks.begin_backward)
+            # GEMM grids on this engine (see _DDPHooks.backward_sched)
             from . import _lib as K
-            K.set_gemm_persistent(False)
+            eng.base_sched = eng.gemm_sched = K.SCHED_NO_PERSISTENT
         self.units = unit_ranges(module.layout, module.config.n_layer)
         self.plans, self.shard_total = plan_shards(self.units, W)
         self.plan = {p.name: p for p in self.plans}
@@ -328,6 +333,9 @@ class FullyShardedDataParallel(nn.Module):
         self._bf16_fresh = False                     # shard_bf16 == bf16(flat_param) (set by our AdamW)
         self._seen_version = None
         self.hooks = _FSDPHooks(self, W)
+        # a torch optimizer on flat_param (fused AdamW does not bump its version): every gathered unit goes stale
+        from .engine import watch_optimizer_steps
+        watch_optimizer_steps(self, [self.flat_param], FullyShardedDataParallel._stale_after_step)
         eng.grad_sync = self.hooks
         eng.param_provider = self.hooks
         eng.zero_grad()
@@ -367,6 +375,9 @@ class FullyShardedDataParallel(nn.Module):
         self._valid = {u: None for u in self.order}
         self._bf16_fresh = bf16_fresh
         self._seen_version = self.flat_param._version
+
+    def _stale_after_step(self):
+        self._seen_version = None  # _check_version then treats every gathered unit as stale
 
     def _check_version(self):
         if self._seen_version is None or self.flat_param._version != self._seen_version:
@@ -446,11 +457,14 @@ class FullyShardedDataParallel(nn.Module):
         # the packed inputs hold this backward's gradients: the full arena restarts from zero
         K.zero_(self.engine.grad)
         self.engine.grad_dirty = False
+        # accumulate only into a gradient the caller still holds: after a torch optimizer's
+        # zero_grad(set_to_none=True) flat_param.grad is None and the shard's old values are stale
+        acc = self.flat_param.grad is self.grad_shard
         for u, work, out in self._rs_works:
             if work is not None:
                 work.wait()
             p = self.plan[u]
-            K.fsdp_accum(out, self.grad_shard[p.soff:p.soff + p.per], p.per, accumulate=True)
+            K.fsdp_accum(out, self.grad_shard[p.soff:p.soff + p.per], p.per, accumulate=acc)
         self._rs_works = []
         self.flat_param.grad = self.grad_shard
 

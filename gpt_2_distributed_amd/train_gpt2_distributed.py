@@ -162,10 +162,15 @@ def main(argv=None):
         model = base
     optim = model.configure_optimizers(weight_decay=0.1, learning_rate=args.lr, betas=(0.9, 0.95))
     global_step, start_epoch, skip = 0, 0, 0
+    # the epoch the DataLoader's persistent workers were spawned with: they keep that dataset copy, so every later
+    # epoch replays its order (SURVEY §5 "epoch freeze"); a resumed run must spawn its workers with the same one
+    worker_epoch = None
     if args.resume:
         st = load_checkpoint(model, optim, args.resume)
         global_step = st["step"]
         start_epoch, skip = int(st.get("epoch", 0)), int(st.get("micro", 0))
+        if "worker_epoch" in st:
+            worker_epoch = int(st["worker_epoch"])
     fpt = 6 * (config.n_layer * 12 * config.n_embd ** 2 + config.vocab_size * config.n_embd) + \
         12 * config.n_layer * args.seq_len * config.n_embd
     optim.zero_grad()
@@ -173,7 +178,12 @@ def main(argv=None):
     t_last, steps_since = time.perf_counter(), 0
     done, epoch, micro = False, start_epoch, 0
     for epoch in range(start_epoch, args.epochs):
-        ds.set_epoch(epoch)  # as the reference; persistent workers keep epoch 0
+        ds.set_epoch(epoch)  # as the reference; persistent workers keep the epoch they were spawned with
+        if dl is not None:
+            if worker_epoch is None:
+                worker_epoch = epoch  # the workers spawn at this epoch's first iteration
+            else:
+                ds.set_epoch(worker_epoch)  # no effect once they run; a resumed run spawns them with it
         if is_primary():
             print(f"\n==== Epoch {epoch} ====")
         batches = dl if dl is not None else gpt2_dataloader.iter_batches(paths, args.seq_len, args.batch, 1,
@@ -211,13 +221,15 @@ def main(argv=None):
                                       "mfu": round(tps * fpt / (world * PEAK_BF16), 4)}), flush=True)
                 t_last, steps_since = now, 0
             if global_step % args.save_every == 0:
-                save_checkpoint(model, optim, global_step, args.save_dir, {"epoch": epoch, "micro": micro})
+                save_checkpoint(model, optim, global_step, args.save_dir,
+                                {"epoch": epoch, "micro": micro, "worker_epoch": worker_epoch})
             if args.max_steps and global_step >= args.max_steps:
                 done = True
                 break
         if done:
             break
     pos = {"epoch": epoch, "micro": micro} if done else {"epoch": args.epochs, "micro": 0}
+    pos["worker_epoch"] = worker_epoch
     save_checkpoint(model, optim, global_step, args.save_dir, pos)
     if dist.is_initialized():
         dist.barrier()

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GPT2MI_ABI_VERSION 7
+#define GPT2MI_ABI_VERSION 8
 
 const char* gpt2mi_last_error(void);
 int gpt2mi_abi_version(void); /* returns GPT2MI_ABI_VERSION of the built library */
@@ -65,19 +65,36 @@ int gpt2mi_colsum_bf16(const uint16_t* g, float* db, int M, int N, int ld, void*
  *          4 GELU_BWD: C = bf16(acc * aux) (aux from the GELU forward)   5 ATOMIC: C fp32 += acc (split-K)
  * dbias (may be NULL; BF16 / GELU_BWD epilogues of layouts 0/1): dbias[n] += sum_m C[m][n] of the stored
  * output — the bias gradient of the Linear whose output grad C is (fused into the 256x256 epilogue).
- * Requires M, N multiples of 128 and K a multiple of 64*splits. */
+ * Requires M, N multiples of 64 and K a multiple of 64*splits (layout 0: any N multiple of 64 and any K-tile count on
+ * the 256x256 kernels; layouts 1 / 2 with N (and M) not multiples of 256 run on the 128x128 kernel).
+ * `sched`: GPT2MI_SCHED_* below. */
 int gpt2mi_gemm(int layout, int epilogue, int M, int N, int K, const uint16_t* A, int lda, const uint16_t* B, int ldb,
                 void* C, int ldc, const float* bias, const float* resid, uint16_t* aux, int ldaux, float alpha,
                 const float* alpha_dev, int accumulate, int splits, float p_drop, uint64_t seed, float* dbias,
-                void* stream);
+                int sched, void* stream);
+
+/* GEMM schedule, chosen per call (v8; v7 had process-global switches):
+ *  GPT2MI_SCHED_AUTO: the library picks the kernel (ping-pong 256x256; its persistent schedule for the short-K
+ *    forward-layout shapes).
+ *  GPT2MI_SCHED_NO_PERSISTENT (flag): never the persistent (one block per CU) schedule. The data-parallel wrappers
+ *    pass it while their RCCL kernels may run concurrently: a persistent block that lands on a CU held by a
+ *    collective waits for it, and the grid ends on its latest block.
+ *  low byte (A/B experiments and the kernel-equivalence tests only): 1 = 128x128 kernel, 2 = 2-stage 256x256,
+ *    3..5 = ping-pong with half-tile map 1..3, 6 = ping-pong one tile per block, 7 = persistent at any K,
+ *    8 = weight gradients on the ping-pong kernel (= auto). */
+#define GPT2MI_SCHED_AUTO 0
+#define GPT2MI_SCHED_NO_PERSISTENT 0x100
 
 /* Weight gradient (train_gpt2_distributed.py:412 autograd wgrad of every nn.Linear):
  * C[M][N] (+)= alpha*(alpha_dev?) * A^T B, A stored [K][M] (dY), B stored [K][N] (X), K = tokens.
  * 256x256 tiles; `splits` K ranges write fp32 partial slabs to `workspace` (>= splits*M*N floats),
- * summed into C in a fixed order (deterministic). M, N multiples of 256; K of 64; ldc == N. */
+ * summed into C in a fixed order (deterministic). M, N, K multiples of 64; ldc == N. sched: as gpt2mi_gemm
+ * (the low byte 2 selects the 2-stage kernel). When M (N) is not a multiple of 256 (GPT-2 1.5B: 1600, 4800) the
+ * partial last tile reads A (B) up to 192 elements past the end of its last row: the caller's allocation must
+ * extend that far (the values are not used). */
 int gpt2mi_gemm_wgrad(int M, int N, int K, const uint16_t* A, int lda, const uint16_t* B, int ldb, float* C, int ldc,
                       int accumulate, float alpha, const float* alpha_dev, float* workspace, size_t workspace_floats,
-                      int splits, void* stream);
+                      int splits, int sched, void* stream);
 
 /* K4-K8: causal flash attention, head_dim 64 — model.py:124-155. q/k/v read from qkv [B*T, 3C];
  * out [B*T, C] head-merged; lse [B*H, T] (natural log of the 1/sqrt(D)-scaled scores). */
@@ -132,14 +149,6 @@ int gpt2mi_colsum_f32(const float* g, float* db, int M, int N, int ld, void* str
 int gpt2mi_xent_fwd_f32(const float* logits, int ld, const int64_t* labels, float* loss_rows, float* lse,
                         float* dlogits, int ldd, int M, int V, int ignore_index, float* loss, float* inv_count,
                         void* stream);
-
-/* GEMM kernel selection for A/B benchmarking: 0 = auto (256x256 tiles for layouts 0/1 when N % 256 == 0),
- * 1 = always the 128x128 kernel. */
-void gpt2mi_set_gemm_impl(int impl);
-/* 1 (default) lets the auto selection use the persistent GEMM schedule (one block per CU walking the tiles); 0 turns
- * it off. The data-parallel wrappers turn it off while their RCCL kernels may run concurrently: a block that lands
- * on a CU held by a collective would wait for it, and a persistent grid ends on its latest block. */
-void gpt2mi_set_gemm_persistent(int on);
 
 /* dst[c][r] = src[r][c] for a bf16 [R][C] matrix (R, C multiples of 64): the transposed weight shadow
  * the backward dgrad GEMMs read in the forward (k-contiguous) layout. */

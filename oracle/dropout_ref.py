@@ -15,6 +15,8 @@ Element indexing per site (the kernels' own):
     (q >> 4) & 1 (`csrc/attention.hip`, `csrc/fp32.hip`).
 keep = int16(uniform16) >= round(p * 2^16) - 2^15, i.e. (uniform16 ^ 0x8000) >= round(p * 2^16): P(keep) = 1 - p
 (a signed threshold, so the attention forward decides a pair with one packed int16 subtract).
+The 64-bit site seed's low word is the additive offset of the first round, its high word (made odd; 0 means
+murmur3's 0x85EBCA6B) the multiplier of the second (`csrc/common.h` seed32 / seed_kx).
 """
 from __future__ import annotations
 
@@ -25,7 +27,13 @@ M32 = np.uint64(0xFFFFFFFF)
 
 
 def seed32(seed: int) -> np.uint32:
-    return np.uint32((seed & 0xFFFFFFFF) ^ ((seed >> 32) & 0xFFFFFFFF))
+    return np.uint32(seed & 0xFFFFFFFF)
+
+
+def seed_kx(seed: int) -> np.uint64:
+    """The second-round multiplier of a site (csrc/common.h seed_kx)."""
+    hi = (seed >> 32) & 0xFFFFFFFF
+    return np.uint64(hi | 1 if hi else 0x85EBCA6B)
 
 
 def threshold(p: float) -> int:
@@ -35,11 +43,11 @@ def threshold(p: float) -> int:
     return int(min(p * 65536.0 + 0.5, 65536.0))
 
 
-def drop_hash(s32: np.uint32, x: np.ndarray) -> np.ndarray:
-    """Two multiply(-xorshift) rounds over uint32 (csrc/common.h drop_hash): ((x + s32) * C1 ^ >> 16) * C2."""
-    h = ((x.astype(np.uint64) + np.uint64(s32)) & M32) * np.uint64(0x9E3779B1) & M32
+def drop_hash(seed: int, x: np.ndarray) -> np.ndarray:
+    """Two multiply(-xorshift) rounds over uint32 (csrc/common.h drop_hash): ((x + s32) * C1 ^ >> 16) * kx."""
+    h = ((x.astype(np.uint64) + np.uint64(seed32(seed))) & M32) * np.uint64(0x9E3779B1) & M32
     h ^= h >> np.uint64(16)
-    return h * np.uint64(0x85EBCA6B) & M32
+    return h * seed_kx(seed) & M32
 
 
 def _keep(h: np.ndarray, half: np.ndarray, thr: int) -> np.ndarray:
@@ -51,7 +59,7 @@ def _keep(h: np.ndarray, half: np.ndarray, thr: int) -> np.ndarray:
 def site_scale(seed: int, rows: int, cols: int, p: float) -> torch.Tensor:
     """keep / (1 - p) multipliers of an [rows, cols] site (embedding, proj, fc1, fc2)."""
     e = np.arange(rows * cols, dtype=np.uint64)
-    keep = _keep(drop_hash(seed32(seed), (e >> np.uint64(1)) & M32), e & np.uint64(1), threshold(p))
+    keep = _keep(drop_hash(seed, (e >> np.uint64(1)) & M32), e & np.uint64(1), threshold(p))
     return torch.from_numpy(keep.reshape(rows, cols).astype(np.float32) / np.float32(1.0 - p))
 
 
@@ -61,7 +69,7 @@ def attn_scale(seed: int, BH: int, T: int, p: float) -> torch.Tensor:
     q = np.arange(T, dtype=np.uint64)[None, :, None]
     k = np.arange(T, dtype=np.uint64)[None, None, :]
     x = ((bh * np.uint64(T) + (q & ~np.uint64(16))) * np.uint64(T) + k) & M32
-    keep = _keep(drop_hash(seed32(seed), x), (q >> np.uint64(4)) & np.uint64(1), threshold(p))
+    keep = _keep(drop_hash(seed, x), (q >> np.uint64(4)) & np.uint64(1), threshold(p))
     return torch.from_numpy(keep.astype(np.float32) / np.float32(1.0 - p))
 
 

@@ -18,6 +18,12 @@ Outputs (all small data files, no reference source):
   ddp_golden.json   the DDP identity: the reference run single-process on the concatenation of two
                     ranks' micro-batches (L=2, C=256, H=4, V=509, T=64; 2 ranks x B=2, grad_accum=2, 3 steps,
                     lr 1e-3): per-step loss and grad norm, and final-parameter checks, for the 2-rank tests.
+  cfg5_golden.json  the same identity at BASELINE cfg 5's widths (GPT-2 1.5B: C=1600, H=25, V=50257) on 2 layers,
+                    T=256, 2 ranks x B=1, grad_accum=2, 2 steps, lr 1e-4, Zipf tokens stored in the file: the FSDP +
+                    gradient-accumulation test of the 1.5B configuration.
+  ddp124_golden.json the same identity at cfg 3's widths (GPT-2 124M: C=768, H=12, V=50257, T=1024) on 2 layers,
+                    2 ranks x B=2, grad_accum=1, 3 steps, lr 1e-3, Zipf tokens stored in the file: the DDP test with
+                    the default 64 MiB buckets.
 """
 from __future__ import annotations
 
@@ -143,6 +149,40 @@ def ddp_golden(steps=3, grad_accum=2, world=2, per_rank=2):
     print("ddp golden", losses, norms)
 
 
+def _wide_golden(name, cfg_kw, seq_len, steps, grad_accum, world, per_rank, lr, seed):
+    """Reference run on the concatenated batch at a production width; the Zipf(1.2) tokens are stored in the file
+    (tokens[s][a][row] = the T+1 tokens of row `row` of micro-batch a of step s; rank r takes rows r*per_rank..)."""
+    cfg = ref_model.GPT2Config(**cfg_kw)
+    rng = np.random.default_rng(seed)
+    toks = (np.minimum(rng.zipf(1.2, size=(steps, grad_accum, world * per_rank, seq_len + 1)), cfg.vocab_size)
+            - 1).astype(np.int64)
+    batches = [(torch.from_numpy(toks[s_, a, :, :-1].copy()), torch.from_numpy(toks[s_, a, :, 1:].copy()))
+               for s_ in range(steps) for a in range(grad_accum)]
+    torch.set_num_threads(8)
+    ms = []
+    t0 = time.time()
+    losses, norms = _ref_traj(cfg, batches, steps, grad_accum=grad_accum, lr=lr, model_out=ms)
+    with open(os.path.join(HERE, name), "w") as f:
+        json.dump({"config": cfg_kw, "world": world, "per_rank": per_rank, "grad_accum": grad_accum, "steps": steps,
+                   "seq_len": seq_len, "lr": lr,
+                   "data": f"np.random.default_rng({seed}).zipf(1.2) clipped to [0, V); stored in 'tokens'",
+                   "tokens": toks.tolist(), "losses": losses, "grad_norms": norms,
+                   "params": _param_checks(ms[0])}, f, indent=0)
+    print(name, losses, norms, f"{time.time() - t0:.1f} s")
+
+
+def cfg5_golden():
+    _wide_golden("cfg5_golden.json", dict(n_layer=2, n_head=25, n_embd=1600, vocab_size=50257, n_positions=256,
+                                          resid_pdrop=0.0, attn_pdrop=0.0),
+                 seq_len=256, steps=2, grad_accum=2, world=2, per_rank=1, lr=1e-4, seed=31)
+
+
+def ddp124_golden():
+    _wide_golden("ddp124_golden.json", dict(n_layer=2, n_head=12, n_embd=768, vocab_size=50257, n_positions=1024,
+                                            resid_pdrop=0.0, attn_pdrop=0.0),
+                 seq_len=1024, steps=3, grad_accum=1, world=2, per_rank=2, lr=1e-3, seed=37)
+
+
 def init_124m():
     cfg = ref_model.GPT2Config(n_layer=12, n_head=12, n_embd=768, n_positions=1024, vocab_size=50257)
     m = ref_model.GPT2(cfg)
@@ -219,7 +259,8 @@ if __name__ == "__main__":
     ap.add_argument("--only", default="")
     a = ap.parse_args()
     jobs = {"tiny": tiny_fwd_bwd, "tinytraj": tiny_traj, "init": init_124m, "loader": loader_grid,
-            "traj": traj_124m, "accum": tiny_accum, "ddp": ddp_golden}
+            "traj": traj_124m, "accum": tiny_accum, "ddp": ddp_golden, "cfg5": cfg5_golden,
+            "ddp124": ddp124_golden}
     for k, fn in jobs.items():
         if a.only and k not in a.only.split(","):
             continue

@@ -126,6 +126,35 @@ def test_custom_loss_on_logits(prec):
         _grads_match(m, params, t_grad)
 
 
+@pytest.mark.parametrize("prec", ["bf16", "fp32"])
+@pytest.mark.parametrize("T", [64, 65, 100])
+def test_reference_loss_idiom_on_returned_logits(prec, T):
+    """The reference forms its loss as F.cross_entropy(logits.view(-1, logits.size(-1)), labels.view(-1))
+    (model.py:357-358): that exact idiom works on the returned logits at any T (the engine pads T to the 64-token
+    attention tile internally), gives the model's own loss (torch's cross-entropy on the bf16 logits vs the
+    fused kernel: 2e-3 under autocast), and backpropagates like it."""
+    import torch.nn.functional as F
+    tol_loss, tol_grad = {"bf16": (2e-3, 2e-2), "fp32": (1e-5, 1e-4)}[prec]
+    m, _, _, _ = _setup()
+    g = torch.Generator().manual_seed(8)
+    idx = torch.randint(0, 509, (2, T), generator=g).to(dev)
+    labels = torch.randint(0, 509, (2, T), generator=g).to(dev)
+    with prec_ctx(prec):
+        logits, loss = m(idx, labels=labels)
+        mine = F.cross_entropy(logits.view(-1, logits.size(-1)), labels.view(-1), ignore_index=-100)
+    assert logits.shape == (2, T, 509)
+    assert abs(mine.item() - loss.item()) <= tol_loss * loss.item()
+    m.zero_grad(set_to_none=True)
+    loss.backward()
+    g_own = m.transformer.h[0].attn.qkv.weight.grad.clone()
+    m.zero_grad(set_to_none=True)
+    with prec_ctx(prec):
+        logits, _ = m(idx)
+        mine = F.cross_entropy(logits.view(-1, logits.size(-1)), labels.view(-1))
+    mine.backward()
+    assert rel_err(m.transformer.h[0].attn.qkv.weight.grad.cpu(), g_own.cpu()) < tol_grad
+
+
 def test_returned_logits_survive_the_next_forward():
     """Each forward returns a fresh logits tensor (the reference returns a new tensor per call)."""
     m, _, _, _ = _setup()

@@ -53,5 +53,20 @@ def test_refuses_shapes_that_overflow_the_dropout_index():
     assert lib.gpt2mi_attn_bwd(None, None, None, None, None, None, None, 256, 1024, 16, 64, 0.1, 1, None) == 22
     # GEMM epilogue dropout: M*N = 2^20 * 2^13 = 2^33 pairs*2
     assert lib.gpt2mi_gemm(0, 2, 1 << 20, 1 << 13, 64, None, 64, None, 64, None, 1 << 13, None, None, None, 0,
-                           1.0, None, 0, 1, 0.1, 1, None, None) == 22
+                           1.0, None, 0, 1, 0.1, 1, None, 0, None) == 22
     assert b"32-bit dropout" in lib.gpt2mi_last_error()
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libgpt2mi.so not built (run __graft_entry__.build())")
+def test_gemm_schedule_is_a_per_call_argument():
+    """ABI v8: the GEMM schedule is passed with every call (no process-global switch is exported); an unknown
+    schedule value is refused before any launch."""
+    from gpt_2_distributed_amd import _lib
+    lib = _lib.load()
+    for gone in ("gpt2mi_set_gemm_impl", "gpt2mi_set_gemm_persistent"):
+        assert not hasattr(ctypes.CDLL(LIB), gone), gone
+    assert lib.gpt2mi_gemm(0, 0, 256, 256, 64, None, 64, None, 64, None, 256, None, None, None, 0,
+                           1.0, None, 0, 1, 0.0, 1, None, 0x200, None) == 22
+    assert b"sched" in lib.gpt2mi_last_error()
+    assert lib.gpt2mi_gemm_wgrad(256, 256, 64, None, 256, None, 256, None, 256, 0, 1.0, None, None, 0, 1, 0x1ff,
+                                 None) == 22

@@ -213,8 +213,9 @@ def test_gemm_rejects_bad_shapes():
 
 
 def test_gemm_half_width_n_tile_epilogues():
-    """N % 128 == 64 (GPT-2 1.5B widths) on the 128x128 kernel: bias / GELU+dropout / residual epilogues
-    write exactly the N valid columns (the padding columns of a wider C stay untouched)."""
+    """N % 128 == 64 (GPT-2 1.5B widths; the 256x256 kernel's partial column tile, 3 K-tiles: its odd-count zero
+    tile): bias / GELU+dropout / residual epilogues write exactly the N valid columns (the padding columns of a
+    wider C stay untouched)."""
     M, N, K = 256, 320, 192
     g = torch.Generator().manual_seed(21)
     A, W = bf(torch.randn(M, K, generator=g)), bf(torch.randn(N, K, generator=g) * 0.1)
@@ -433,14 +434,12 @@ def test_gemm256_matches_gemm128(layout, epi):
     resid = torch.randn(M, N, generator=g).to(dev)
     outs = []
     for impl in (0, 1, 2):
-        L().set_gemm_impl(impl)
         f32 = epi == 2
         C = torch.zeros(M, N, device=dev, dtype=torch.float32 if f32 else torch.bfloat16)
         aux = bf(torch.randn(M, N, generator=torch.Generator().manual_seed(5))).to(dev)
         L().gemm(layout, epi, M, N, K, A, K, Bm, ldb, C, N, bias=bias if layout == 0 else None,
-                 resid=resid if epi == 2 else None, aux=aux, ldaux=N, p_drop=0.1, seed=77)
+                 resid=resid if epi == 2 else None, aux=aux, ldaux=N, p_drop=0.1, seed=77, sched=impl)
         outs.append((C.float().cpu(), aux.float().cpu()))
-    L().set_gemm_impl(0)
     for o in outs[1:]:
         assert rel_err(outs[0][0], o[0]) < 1e-5 if epi == 2 else rel_err(outs[0][0], o[0]) < 2e-3
         assert rel_err(outs[0][1], o[1]) < 2e-3
@@ -522,7 +521,7 @@ def test_transpose_bf16_batched():
 def test_gemm_persistent_schedule_bitwise(epi, M, N):
     """The persistent ping-pong schedule (short-K forward-layout GEMMs with >= 2 tiles per CU: one block per CU
     walks the tiles, the next tile's first K-tile lands during this tile's epilogue) computes every output
-    element exactly as the one-tile-per-block kernel (gpt2mi_set_gemm_impl(6) forces that one): bitwise equal,
+    element exactly as the one-tile-per-block kernel (sched 6 forces that one): bitwise equal,
     and within bf16 rounding of an fp32 reference on sampled rows. Covers every epilogue the step runs on it:
     plain / bias (qkv, proj dgrad), GELU + dropout (fc1), fp32 residual + dropout (proj forward) and the GELU
     derivative product with its fused bias gradient (fc2 dgrad; column sums by atomics, so to fp32 rounding)."""
@@ -534,30 +533,26 @@ def test_gemm_persistent_schedule_bitwise(epi, M, N):
     resid = torch.randn(M, N, generator=g).to(dev) if epi == "resid_drop" else None
     dgelu = bf(torch.rand(M, N, generator=g) * 1.2 - 0.1).to(dev) if epi == "gelu_bwd_dbias" else None
     outs, dbs = [], []
-    for impl, persistent in ((0, True), (6, True), (0, False)):  # (0, False): the wrappers' no-persistent switch
-        L().set_gemm_impl(impl)
-        L().set_gemm_persistent(persistent)
-        try:
-            C = torch.empty(M, N, dtype=torch.float32 if epi == "resid_drop" else torch.bfloat16, device=dev)
-            if epi == "gelu_drop":
-                aux = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
-                L().gemm(0, L().EPI_GELU, M, N, K, A, K, W, K, C, N, bias=bias, aux=aux, ldaux=N, p_drop=0.1,
-                         seed=99)
-                outs.append((C, aux))
-            elif epi == "resid_drop":
-                L().gemm(0, L().EPI_RESID, M, N, K, A, K, W, K, C, N, bias=bias, resid=resid, p_drop=0.1, seed=98)
-                outs.append((C,))
-            elif epi == "gelu_bwd_dbias":
-                db = torch.zeros(N, device=dev)
-                L().gemm(0, L().EPI_GELU_BWD, M, N, K, A, K, W, K, C, N, aux=dgelu, ldaux=N, dbias=db)
-                outs.append((C,))
-                dbs.append(db)
-            else:
-                L().gemm(0, L().EPI_BF16, M, N, K, A, K, W, K, C, N, bias=bias)
-                outs.append((C,))
-        finally:
-            L().set_gemm_impl(0)
-            L().set_gemm_persistent(True)
+    # (0, NO_PERSISTENT): the data-parallel wrappers' schedule
+    for sched in (L().SCHED_AUTO, 6, L().SCHED_NO_PERSISTENT):
+        C = torch.empty(M, N, dtype=torch.float32 if epi == "resid_drop" else torch.bfloat16, device=dev)
+        if epi == "gelu_drop":
+            aux = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+            L().gemm(0, L().EPI_GELU, M, N, K, A, K, W, K, C, N, bias=bias, aux=aux, ldaux=N, p_drop=0.1,
+                     seed=99, sched=sched)
+            outs.append((C, aux))
+        elif epi == "resid_drop":
+            L().gemm(0, L().EPI_RESID, M, N, K, A, K, W, K, C, N, bias=bias, resid=resid, p_drop=0.1, seed=98,
+                     sched=sched)
+            outs.append((C,))
+        elif epi == "gelu_bwd_dbias":
+            db = torch.zeros(N, device=dev)
+            L().gemm(0, L().EPI_GELU_BWD, M, N, K, A, K, W, K, C, N, aux=dgelu, ldaux=N, dbias=db, sched=sched)
+            outs.append((C,))
+            dbs.append(db)
+        else:
+            L().gemm(0, L().EPI_BF16, M, N, K, A, K, W, K, C, N, bias=bias, sched=sched)
+            outs.append((C,))
     torch.cuda.synchronize()
     for other in outs[1:]:
         for a, b in zip(outs[0], other):
@@ -575,22 +570,18 @@ def test_gemm_persistent_schedule_bitwise(epi, M, N):
 
 @pytest.mark.parametrize("m,n,tokens,splits", [(2304, 768, 8192, 4), (768, 3072, 8192, 8), (50432, 768, 4096, 3)])
 def test_wgrad_kernels_bitwise(m, n, tokens, splits):
-    """The weight gradient on the ping-pong kernel (default), the 2-stage 256x256 kernel (impl 2) and the 5-slot
-    ring kernel (impl 9): the same K order per output element (split counts chosen so every kernel cuts K at the
-    same K-tiles), so bitwise equal; and within fp32 rounding of a float64 reference on sampled rows."""
+    """The weight gradient on the ping-pong kernel (default) and the 2-stage 256x256 kernel (sched 2): the same K
+    order per output element (split counts chosen so both kernels cut K at the same K-tiles), so bitwise equal; and
+    within fp32 rounding of a float64 reference on sampled rows."""
     g = torch.Generator().manual_seed(m + n + splits)
     A = bf(torch.randn(tokens, m, generator=g) * 0.1).to(dev)
     B = bf(torch.randn(tokens, n, generator=g)).to(dev)
     ws = torch.empty(splits * m * n, device=dev)
     outs = []
-    for impl in (0, 2, 9):
-        L().set_gemm_impl(impl)
-        try:
-            C = torch.zeros(m, n, device=dev)
-            L().gemm_wgrad(m, n, tokens, A, m, B, n, C, n, accumulate=True, workspace=ws, splits=splits)
-            outs.append(C)
-        finally:
-            L().set_gemm_impl(0)
+    for impl in (0, 2):
+        C = torch.zeros(m, n, device=dev)
+        L().gemm_wgrad(m, n, tokens, A, m, B, n, C, n, accumulate=True, workspace=ws, splits=splits, sched=impl)
+        outs.append(C)
     torch.cuda.synchronize()
     for o in outs[1:]:
         assert torch.equal(outs[0], o)
@@ -598,3 +589,89 @@ def test_wgrad_kernels_bitwise(m, n, tokens, splits):
     ref = A[:, rows].double().t() @ B.double()
     err = (outs[0][rows].double() - ref).abs().max().item() / ref.abs().max().item()
     assert err < 1e-5, err
+
+
+def _tail(t):
+    """t's values in a buffer with 256 elements of slack past its end (the weight-gradient GEMM's partial-tile reads,
+    gpt2mi.h gpt2mi_gemm_wgrad; the engine allocates its activations so)."""
+    buf = torch.full((t.numel() + 256,), float("nan"), dtype=t.dtype, device=dev)
+    out = buf[:t.numel()].view(t.shape)
+    out.copy_(t.to(dev))
+    return out
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 1600, 1600), (256, 4800, 1600), (320, 1600, 4800), (256, 6400, 1600),
+                                   (512, 1600, 6400), (64, 64, 128), (256, 320, 192)])
+def test_gemm_edge_tiles_and_odd_k_vs_fp64(M, N, K):
+    """GPT-2 1.5B's GEMM shapes on the ping-pong kernel: N a multiple of 64 but not of 256 (a partial last column
+    tile: 1600 = 6.25 x 256, 4800 = 18.75 x 256) and odd K-tile counts (K = 1600: 25, 4800: 75; run as a zero K-tile
+    plus the rest). fp32 output with alpha and accumulate against float64; the columns of a wider C past N stay
+    untouched."""
+    g = torch.Generator().manual_seed(M + N + K)
+    A = bf(torch.randn(M, K, generator=g))
+    W = bf(torch.randn(N, K, generator=g))
+    C0 = torch.randn(M, N, generator=g)
+    ref = C0.double() + 0.25 * (A.double() @ W.double().t())
+    ld = N + 64
+    C = torch.full((M, ld), 7.0, device=dev)
+    C[:, :N] = C0.to(dev)
+    L().gemm(0, L().EPI_F32, M, N, K, A.to(dev), K, W.to(dev), K, C, ld, alpha=0.25, accumulate=True)
+    torch.cuda.synchronize()
+    assert rel_err(C[:, :N].cpu(), ref) < 1e-6
+    assert torch.all(C[:, N:] == 7.0)
+
+
+@pytest.mark.parametrize("N,K", [(1600, 1600), (4800, 1600), (1600, 4800)])
+def test_gemm_edge_epilogues_vs_oracle(N, K):
+    """The fused epilogues the 1.5B step runs on partial column tiles: bias (qkv), fp32 residual + dropout (proj /
+    fc2: the oracle's own mask of the site), GELU + dropout with its masked derivative (fc1 at K = 1600), and the
+    GELU-derivative product with the fused bias gradient (fc2 dgrad)."""
+    from oracle import dropout_ref as D
+    M = 512
+    g = torch.Generator().manual_seed(N + 3 * K)
+    A, W = bf(torch.randn(M, K, generator=g)), bf(torch.randn(N, K, generator=g) * 0.03)
+    bias, resid = torch.randn(N, generator=g), torch.randn(M, N, generator=g)
+    acc = A.double() @ W.double().t()
+    Ad, Wd, bd = A.to(dev), W.to(dev), bias.to(dev)
+    p, seed = 0.1, (0x8CF69C6F << 32) | 12345
+    mask = D.site_scale(seed, M, N, p).double()
+    C = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    L().gemm(0, L().EPI_BF16, M, N, K, Ad, K, Wd, K, C, N, bias=bd)
+    assert rel_err(C.cpu().double(), acc + bias.double()) < 4e-3
+    Cr = torch.empty(M, N, device=dev)
+    L().gemm(0, L().EPI_RESID, M, N, K, Ad, K, Wd, K, Cr, N, bias=bd, resid=resid.to(dev), p_drop=p, seed=seed)
+    assert rel_err(Cr.cpu().double(), resid.double() + (acc + bias.double()) * mask) < 1e-5
+    H = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    G = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    L().gemm(0, L().EPI_GELU, M, N, K, Ad, K, Wd, K, H, N, bias=bd, aux=G, ldaux=N, p_drop=p, seed=seed)
+    u = (acc + bias.double()).float().requires_grad_(True)
+    (model_ref.gelu_tanh(u) * mask.float()).sum().backward()
+    assert rel_err(H.cpu().double(), model_ref.gelu_tanh(u.detach()).double() * mask) < 4e-3
+    assert rel_err(G.cpu().double(), u.grad.double()) < 4e-3
+    db = torch.zeros(N, device=dev)
+    Cg = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    L().gemm(0, L().EPI_GELU_BWD, M, N, K, Ad, K, Wd, K, Cg, N, aux=G, ldaux=N, dbias=db)
+    assert rel_err(Cg.cpu().double(), acc * G.cpu().double()) < 4e-3
+    assert rel_err(db.cpu(), Cg.float().sum(0).cpu()) < 1e-4
+
+
+@pytest.mark.parametrize("m,n,tokens,splits", [(4800, 1600, 4096, 3), (1600, 1600, 2048, 1), (1600, 6400, 2048, 2),
+                                               (6400, 1600, 1024, 1), (50432, 1600, 512, 1), (320, 192, 1024, 4)])
+def test_gemm_wgrad_edge_tiles_vs_fp64(m, n, tokens, splits):
+    """The weight gradients of GPT-2 1.5B (out x in = 4800 x 1600, 1600 x 1600, 1600 x 6400, 6400 x 1600, the tied
+    lm_head 50432 x 1600) on the ping-pong kernel with partial last row / column tiles, split-K slabs or one pass,
+    write (accumulate=False: the lazy-zeroed arena) and accumulate, against float64 on sampled rows."""
+    g = torch.Generator().manual_seed(m + n + tokens)
+    A = _tail(bf(torch.randn(tokens, m, generator=g) * 0.1))
+    B = _tail(bf(torch.randn(tokens, n, generator=g)))
+    ws = torch.empty(max(4, splits * m * n), device=dev)
+    C = torch.full((m, n), float("nan"), device=dev)
+    L().gemm_wgrad(m, n, tokens, A, m, B, n, C, n, accumulate=False, alpha=0.5, workspace=ws, splits=splits)
+    C1 = C.clone()
+    L().gemm_wgrad(m, n, tokens, A, m, B, n, C, n, accumulate=True, alpha=0.5, workspace=ws, splits=splits)
+    torch.cuda.synchronize()
+    rows = torch.cat([torch.arange(0, m, max(1, m // 24), device=dev), torch.arange(m - 8, m, device=dev)])
+    ref = 0.5 * (A[:, rows].double().t() @ B.double())
+    assert rel_err(C1[rows].double().cpu(), ref.cpu()) < 1e-5
+    assert rel_err(C[rows].double().cpu(), 2 * ref.cpu()) < 1e-5
+    assert not torch.isnan(C).any()

@@ -117,6 +117,33 @@ def test_torch_optimizer_and_clip_grad_norm_interop():
     assert rel_err(a.arena.cpu(), b.arena.cpu()) < 2e-3  # fp32 rounding of two AdamW implementations, 3 steps
 
 
+@pytest.mark.parametrize("fused", [False, True])
+def test_torch_fused_adamw_under_autocast_refreshes_the_shadow(fused):
+    """The reference trainer's exact optimizer, torch.optim.AdamW(fused=True) (train_gpt2_distributed.py:356-362), under
+    bf16 autocast: torch's fused kernel updates the parameters without bumping their version counters, so the engine
+    learns of the step from a global optimizer post-step hook and re-casts its bf16 GEMM shadow; the trajectory then
+    follows the repo's fused AdamW on the same model."""
+    g = np.load(os.path.join(GOLDEN, "tiny_fwd_bwd.npz"))
+    idx = torch.from_numpy(g["idx"]).to(dev)
+    labels = torch.from_numpy(g["labels"]).to(dev)
+    a, b = _tiny_model(), _tiny_model()
+    oa = torch.optim.AdamW(a.parameters(), lr=1e-3, weight_decay=0.1, betas=(0.9, 0.95), fused=fused)
+    ob = b.configure_optimizers(learning_rate=1e-3)
+    for _ in range(4):
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            _, la = a(idx, labels=labels)
+        la.backward()
+        oa.step()
+        oa.zero_grad()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            _, lb = b(idx, labels=labels)
+        lb.backward()
+        ob.step()
+        ob.zero_grad()
+        assert abs(la.item() - lb.item()) < 2e-3 * la.item()
+    assert rel_err(a.arena.cpu(), b.arena.cpu()) < 2e-3
+
+
 def test_grad_accumulation_equals_big_batch():
     g = np.load(os.path.join(GOLDEN, "tiny_fwd_bwd.npz"))
     idx = torch.from_numpy(g["idx"]).to(dev)

@@ -104,26 +104,32 @@ def test_124m_trajectory_first_steps():
     np.testing.assert_allclose(norms, ref["grad_norms"][:3], rtol=1e-3)
 
 
+def _h_py(seed, x):
+    """Scalar pure-python restatement of csrc/common.h drop_hash(seed32(seed), seed_kx(seed), x)."""
+    s, hi = seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF
+    kx = (hi | 1) if hi else 0x85EBCA6B
+    h = (((x + s) & 0xFFFFFFFF) * 0x9E3779B1) & 0xFFFFFFFF
+    h ^= h >> 16
+    return (h * kx) & 0xFFFFFFFF
+
+
 def test_dropout_restatement():
     """oracle/dropout_ref.py: numpy hash == a scalar pure-python restatement; drop rate p; pair layout;
     the oracle forward with all-ones masks == dropout 0."""
     from oracle import dropout_ref as D
+    from gpt_2_distributed_amd.engine import site_seeds
 
-    def h_py(s, x):
-        h = (((x + s) & 0xFFFFFFFF) * 0x9E3779B1) & 0xFFFFFFFF
-        h ^= h >> 16
-        return (h * 0x85EBCA6B) & 0xFFFFFFFF
-
-    seed = 0x0123456789ABCDEF
-    s32 = int(D.seed32(seed))
-    assert s32 == (0x89ABCDEF ^ 0x01234567)
+    seed = site_seeds(1234, 7, 2)[("attn", 1)]
+    assert int(D.seed32(seed)) == seed & 0xFFFFFFFF and int(D.seed_kx(seed)) == (seed >> 32) | 1
+    assert int(D.seed_kx(77)) == 0x85EBCA6B  # a zero high word takes murmur3's multiplier
     xs = np.array([0, 1, 2, 12345, 2**31 + 7, 2**32 - 1], dtype=np.uint64)
-    assert [int(v) for v in D.drop_hash(D.seed32(seed), xs)] == [h_py(s32, int(x)) for x in xs]
+    for sd in (seed, 77):
+        assert [int(v) for v in D.drop_hash(sd, xs)] == [_h_py(sd, int(x)) for x in xs]
     assert D.threshold(0.1) == 6554 and D.threshold(0.0) == 0
     # no correlation between the decisions of neighbouring counters along the strides the kernels walk
     # (adjacent keys, the next query row at T = 1024, the next 32-query half, the paired query q ^ 16)
     x = np.arange(1 << 20, dtype=np.uint64) * np.uint64(3) + np.uint64(977)
-    keep = lambda idx, half: D._keep(D.drop_hash(np.uint32(s32), idx), np.full(idx.shape, half), 6554)  # noqa
+    keep = lambda idx, half: D._keep(D.drop_hash(seed, idx), np.full(idx.shape, half), 6554)  # noqa
     for h0 in (0, 1):
         base = keep(x, h0).astype(np.float64)
         for stride, half in ((1, 0), (1, 1), (2, 0), (16, 1), (1024, 0), (1024, 1), (32 * 1024, 0), (1 << 16, 1),
@@ -135,7 +141,7 @@ def test_dropout_restatement():
     assert torch.allclose(m[m > 0], torch.tensor(1 / 0.9))
     # elements 2j, 2j+1 share hash j: halves 0 / 1
     e = np.arange(16, dtype=np.uint64)
-    hv = D.drop_hash(D.seed32(seed), e >> np.uint64(1))
+    hv = D.drop_hash(seed, e >> np.uint64(1))
     half16 = (hv >> (np.uint64(16) * (e & np.uint64(1)))) & np.uint64(0xFFFF)
     keep = half16.astype(np.uint16).view(np.int16).astype(np.int64) >= 6554 - 32768  # signed threshold
     assert np.array_equal(keep, (m.reshape(-1)[:16] > 0).numpy())
@@ -144,7 +150,7 @@ def test_dropout_restatement():
     # queries q and q^16 of one key share a hash: (q & ~16)
     q, k = 3, 40
     x = (1 * 64 + (q & ~16)) * 64 + k
-    hh = h_py(s32, x)
+    hh = _h_py(seed, x)
     s16 = lambda v: v - 65536 if v >= 32768 else v  # noqa: E731
     assert (a[1, q, k] > 0).item() == (s16(hh & 0xFFFF) >= 6554 - 32768)
     assert (a[1, q ^ 16, k] > 0).item() == (s16((hh >> 16) & 0xFFFF) >= 6554 - 32768)
@@ -154,6 +160,43 @@ def test_dropout_restatement():
     l0, _ = model_ref.forward(params, TINY, idx, None, "fp32")
     l1, _ = model_ref.forward(params, TINY, idx, None, "fp32", drop=ones)
     assert torch.equal(l0, l1)
+
+
+def test_dropout_sites_are_independent():
+    """the sites of a step draw distinct decision streams. With one multiplier for every site, site
+    s's mask at counter x equals site s''s at x + (s - s'): the same decisions reused, shifted. The engine's seeds give
+    every site of a step its own vetted multiplier (dropout_keys.py), so the keep decisions of two sites are
+    uncorrelated both at equal counters and at the counter shift that maps one site's first round onto the other's.
+    Checked for adjacent and distant site pairs of a 48-layer (GPT-2 1.5B) step, both 16-bit halves."""
+    from oracle import dropout_ref as D
+    from gpt_2_distributed_amd.dropout_keys import MULTIPLIERS
+    from gpt_2_distributed_amd.engine import site_seeds
+
+    seeds = site_seeds(1234, 3, 48)
+    keys = list(seeds)
+    assert len({s >> 32 for s in seeds.values()}) == len(seeds) == 193  # one multiplier per site
+    assert len(set(MULTIPLIERS)) == len(MULTIPLIERS) and all(m & 1 for m in MULTIPLIERS)
+    x = np.arange(1 << 19, dtype=np.uint64)
+    M32 = np.uint64(0xFFFFFFFF)
+    worst = 0.0
+    pairs = [(keys[i], keys[i + 1]) for i in range(0, 40, 3)] + [(keys[0], keys[-1]), (keys[5], keys[100])]
+    for a, b in pairs:
+        sa, sb = seeds[a], seeds[b]
+        shift = np.uint64(((sa & 0xFFFFFFFF) - (sb & 0xFFFFFFFF)) & 0xFFFFFFFF)
+        ha = D.drop_hash(sa, x)
+        for xb in (x, (x + shift) & M32):  # equal counters; the translate of the shared-multiplier hash
+            hb = D.drop_hash(sb, xb)
+            for half in (0, 1):
+                hv = np.full(x.shape, half)
+                ka = D._keep(ha, hv, 6554).astype(np.float64)
+                kb = D._keep(hb, hv, 6554).astype(np.float64)
+                worst = max(worst, abs(float(np.corrcoef(ka, kb)[0, 1])))
+    assert worst < 0.01, worst
+    # the shared-multiplier hash (one multiplier, additive site key: the round-2 design) fails this check
+    same = lambda s: (0x85EBCA6B << 32) | (s & 0xFFFFFFFF)  # noqa: E731
+    sa, sb = same(seeds[keys[0]]), same(seeds[keys[1]])
+    shift = np.uint64(((sa & 0xFFFFFFFF) - (sb & 0xFFFFFFFF)) & 0xFFFFFFFF)
+    assert np.array_equal(D.drop_hash(sa, x), D.drop_hash(sb, (x + shift) & M32))
 
 
 def _check_params(params, ref, rtol):
@@ -187,6 +230,24 @@ def test_ddp_golden_is_the_concatenated_batch_run():
     S, GA, W, P = ref["steps"], ref["grad_accum"], ref["world"], ref["per_rank"]
     toks = torch.randint(0, 509, (S, GA, W * P, 65), generator=torch.Generator().manual_seed(5))
     batches = [(toks[s, a, :, :-1].contiguous(), toks[s, a, :, 1:].contiguous()) for s in range(S) for a in range(GA)]
+    params = model_ref.init_params(cfg)
+    losses, norms = train_ref.run(cfg, batches, S, grad_accum=GA, lr=ref["lr"], params=params)
+    np.testing.assert_allclose(losses, ref["losses"], rtol=1e-4)
+    np.testing.assert_allclose(norms, ref["grad_norms"], rtol=1e-3)
+    _check_params(params, ref["params"], 1e-4)
+
+
+@pytest.mark.parametrize("name", ["cfg5_golden.json", "ddp124_golden.json"])
+def test_production_width_goldens_match_the_oracle(name):
+    """The production-width goldens (the reference on the concatenated batch at GPT-2 1.5B widths with grad_accum 2,
+    and at 124M widths with T=1024) are what the oracle's loop computes from the stored tokens: pins the oracle at
+    the widths of BASELINE cfgs 3 and 5 (H=25 heads, C=1600, the full vocabulary)."""
+    ref = json.load(open(os.path.join(GOLDEN, name)))
+    cfg = model_ref.Cfg(**ref["config"])
+    S, GA = ref["steps"], ref["grad_accum"]
+    toks = torch.tensor(ref["tokens"], dtype=torch.int64)
+    batches = [(toks[s, a, :, :-1].contiguous(), toks[s, a, :, 1:].contiguous()) for s in range(S) for a in range(GA)]
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
     params = model_ref.init_params(cfg)
     losses, norms = train_ref.run(cfg, batches, S, grad_accum=GA, lr=ref["lr"], params=params)
     np.testing.assert_allclose(losses, ref["losses"], rtol=1e-4)

@@ -112,6 +112,31 @@ def test_trainer_cli_resume_skips_consumed_batches(tmp_path):
     assert abs(resumed[3] - full[2]) <= 1e-4 * full[2] and abs(resumed[4] - full[3]) <= 1e-4 * full[3]
 
 
+def test_trainer_cli_resume_in_a_later_epoch(tmp_path):
+    """Resume inside epoch 1 with DataLoader workers: the persistent workers replay the order they were
+    spawned with (epoch 0), so the resumed run must spawn its workers with that epoch, not the one it
+    resumes in. 11 batches per epoch, 2 micro-batches per step: step 7 ends inside epoch 1; steps 8-9 after a resume
+    from it log the uninterrupted run's losses."""
+    data = tmp_path / "data"
+    base = [sys.executable, "-m", "gpt_2_distributed_amd.train_gpt2_distributed", "--data_dir", str(data),
+            "--synthetic", "2", "--synthetic_tokens", "3000", "--seq_len", "128", "--batch", "4",
+            "--grad_accum_steps", "2", "--workers", "1", "--log_every", "1", "--training_mode", "local",
+            "--epochs", "3", "--max_steps", "9"]
+    r = subprocess.run(base + ["--save_every", "7", "--save_dir", str(tmp_path / "a")], cwd=REPO,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    full = {json.loads(l)["step"]: json.loads(l)["loss"] for l in r.stdout.splitlines() if l.startswith("{")}
+    st = json.load(open(tmp_path / "a" / "step_0000007" / "trainer.json"))
+    assert (st["epoch"], st["worker_epoch"]) == (1, 0), st
+    r = subprocess.run(base + ["--save_every", "100", "--save_dir", str(tmp_path / "b"),
+                               "--resume", str(tmp_path / "a" / "step_0000007")], cwd=REPO, capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    resumed = {json.loads(l)["step"]: json.loads(l)["loss"] for l in r.stdout.splitlines() if l.startswith("{")}
+    for s in (8, 9):
+        assert abs(resumed[s] - full[s]) <= 1e-4 * full[s], (s, resumed, full)
+
+
 def test_trainer_cli_end_to_end(tmp_path):
     """python -m gpt_2_distributed_amd.train_gpt2_distributed with the reference's flags on synthetic
     shards: runs, logs JSON steps with a finite loss, and writes the checkpoint layout."""

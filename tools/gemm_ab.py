@@ -1,5 +1,5 @@
 #!/usr/bin/env python
-"""A/B of GEMM schedules on the GPT-2 124M step shapes (B=64, T=1024): gpt2mi_set_gemm_impl variants timed in
+"""A/B of GEMM schedules on the GPT-2 124M step shapes (B=64, T=1024): gpt2mi_gemm sched variants timed in
 interleaved rounds with HIP events (random data).  python tools/gemm_ab.py [impl_a impl_b ...]  (default 0 6:
 the persistent ping-pong schedule vs the one-tile-per-block kernel)."""
 import os
@@ -46,10 +46,10 @@ def main():
     for _ in range(5):
         for name, (N, W, bias, out, aux, epi, Kd) in bufs.items():
             for impl in impls:
-                K.set_gemm_impl(impl)
                 xa = xs[Kd]
                 fn = lambda: K.gemm(K.FWD, epi, M, N, Kd, xa, Kd, W, Kd, out, N, bias=bias, aux=aux,  # noqa: E731
-                                    ldaux=N if aux is not None else 0, p_drop=0.1 if aux is not None else 0.0, seed=5)
+                                    ldaux=N if aux is not None else 0, p_drop=0.1 if aux is not None else 0.0, seed=5,
+                                    sched=impl)
                 fn()
                 s, e = ev(), ev()
                 s.record()
@@ -58,7 +58,6 @@ def main():
                 e.record()
                 torch.cuda.synchronize()
                 res[(name, impl)].append(s.elapsed_time(e) / 10)
-    K.set_gemm_impl(0)
     for name, (N, *_r) in bufs.items():
         Kd = bufs[name][-1]
         line = f"{name:20s}"

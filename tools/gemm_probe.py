@@ -47,14 +47,14 @@ SHAPES = {
 }
 
 
-def make(layout, epi, M, N, Kd):
+def make(layout, epi, M, N, Kd, sched=0):
     if layout == 2:
         A = (torch.rand(Kd, M, device=dev) * 2 - 1).to(torch.bfloat16)
         B = (torch.rand(Kd, N, device=dev) * 2 - 1).to(torch.bfloat16)
         C = torch.zeros(M, N, device=dev)
         sp = K.wgrad_splits(M, N, Kd)
         ws = torch.empty(max(4, sp * M * N if sp > 1 else 4), device=dev)
-        return lambda: K.gemm_wgrad(M, N, Kd, A, M, B, N, C, N, workspace=ws, splits=sp)
+        return lambda: K.gemm_wgrad(M, N, Kd, A, M, B, N, C, N, workspace=ws, splits=sp, sched=sched)
     A = (torch.rand(M, Kd, device=dev) * 2 - 1).to(torch.bfloat16)
     B = (torch.rand(N, Kd, device=dev) * 2 - 1).to(torch.bfloat16) if layout == 0 else \
         (torch.rand(Kd, N, device=dev) * 2 - 1).to(torch.bfloat16)
@@ -64,7 +64,8 @@ def make(layout, epi, M, N, Kd):
     resid = torch.zeros(M, N, device=dev) if epi == K.EPI_RESID else None
     aux = torch.empty(M, N, device=dev, dtype=torch.bfloat16) if epi in (K.EPI_GELU, K.EPI_GELU_BWD) else None
     ldb = Kd if layout == 0 else N
-    return lambda: K.gemm(layout, epi, M, N, Kd, A, Kd, B, ldb, C, N, bias=bias, resid=resid, aux=aux, ldaux=N)
+    return lambda: K.gemm(layout, epi, M, N, Kd, A, Kd, B, ldb, C, N, bias=bias, resid=resid, aux=aux, ldaux=N,
+                          sched=sched)
 
 
 def main():
@@ -79,13 +80,13 @@ def main():
     K.load()
     for name in names:
         layout, epi, M, N, Kd = SHAPES[name]
-        fn = make(layout, epi, M, N, Kd)
+        fns = {i: make(layout, epi, M, N, Kd, sched=i) for i in impls}
         flop = 2.0 * M * N * Kd
         reps = max(3, int(2e13 / flop))
         res = {i: [] for i in impls}
         for rnd in range(5):
             for i in impls:
-                K.set_gemm_impl(i)
+                fn = fns[i]
                 fn()
                 torch.cuda.synchronize()
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -95,7 +96,6 @@ def main():
                 e.record()
                 torch.cuda.synchronize()
                 res[i].append(s.elapsed_time(e) / reps)
-        K.set_gemm_impl(0)
         line = f"{name:11s} M={M} N={N} K={Kd}:"
         for i in impls:
             ms = sorted(res[i])[len(res[i]) // 2]

@@ -44,7 +44,7 @@ def attn(B=64, T=1024, H=12, p=0.0):
     print(f"attn p={p}: fwd {f:.3f} ms {fl/f/1e9:.0f} TF | bwd {b:.3f} ms {2.5*fl/b/1e9:.0f} TF(2.5x fwd flop)")
 
 
-def gemm(M=65536):
+def gemm(M=65536, sched=0):
     C = 768
     shapes = [
         ("qkv fwd", 0, K.EPI_BF16, M, 3 * C, C),
@@ -80,11 +80,11 @@ def gemm(M=65536):
         if lay == 2 and m % 256 == 0:
             sp = K.wgrad_splits(m, n, k)
             wsb = torch.empty(max(4, sp * m * n if sp > 1 else 4), device=dev)
-            fn = lambda: K.gemm_wgrad(m, n, k, A, lda, Bm, ldb, Cm, n, workspace=wsb, splits=sp)  # noqa
+            fn = lambda: K.gemm_wgrad(m, n, k, A, lda, Bm, ldb, Cm, n, workspace=wsb, splits=sp, sched=sched)  # noqa
         else:
             fn = lambda: K.gemm(lay, epi, m, n, k, A, lda, Bm, ldb, Cm, n, bias=bias if lay == 0 else None,  # noqa
                                 resid=resid, aux=aux, ldaux=n, splits=splits,
-                                p_drop=0.1 if epi in (K.EPI_GELU, K.EPI_RESID) else 0.0, seed=7)
+                                p_drop=0.1 if epi in (K.EPI_GELU, K.EPI_RESID) else 0.0, seed=7, sched=sched)
         ms = timeit(fn, reps=10)
         tf = 2.0 * m * n * k / ms / 1e9
         print(f"{name:16s} M={m:6d} N={n:6d} K={k:6d}: {ms:7.3f} ms {tf:6.0f} TF ({tf/PEAK*100:4.1f}%)")
@@ -145,6 +145,4 @@ if __name__ == "__main__":
         impls = [int(a[5:]) for a in sys.argv[1:] if a.startswith("impl=")] or [0, 2]
         for impl in impls:
             print(f"--- gemm impl {impl} ({ {0: 'ping-pong 256x256', 1: '128x128 only', 2: '2-stage 256x256'}[impl] })")
-            K.set_gemm_impl(impl)
-            gemm()
-        K.set_gemm_impl(0)
+            gemm(sched=impl)

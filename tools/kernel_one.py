@@ -1,7 +1,8 @@
 """Launch ONE of bench.py's probed kernels a few times on step-shaped inputs (GPT-2 124M, B=64, T=1024,
 dropout 0.1), for the rocprofv3 --pmc traffic passes (tools/pmc_traffic.sh -> profiles/traffic.json).
 
-    python tools/kernel_one.py <lm_head_fwd|lm_head_dgrad|lm_head_wgrad|fc1_fwd|attn_fwd|attn_bwd|wgrad> [reps]
+    python tools/kernel_one.py <lm_head_fwd|lm_head_dgrad|lm_head_wgrad|fc1_fwd|proj_fwd|fc2_fwd|qkv_fwd|fc2_dgrad|
+                                attn_fwd|attn_bwd|wgrad> [reps]
 """
 import os
 import sys
@@ -37,6 +38,24 @@ def make(name):
         h, dg = (torch.empty(M, 4 * C, dtype=torch.bfloat16, device=dev) for _ in range(2))
         return lambda: K.gemm(K.FWD, K.EPI_GELU, M, 4 * C, C, a, C, w, C, h, 4 * C, bias=bias, aux=dg, ldaux=4 * C,
                               p_drop=0.1, seed=3)
+    if name == "proj_fwd":  # fp32 residual + dropout epilogue, K = 768
+        a, w, res = r(M, C), r(C, C), torch.randn(M, C, device=dev)
+        bias, out = torch.zeros(C, device=dev), torch.empty(M, C, device=dev)
+        return lambda: K.gemm(K.FWD, K.EPI_RESID, M, C, C, a, C, w, C, out, C, bias=bias, resid=res, p_drop=0.1, seed=4)
+    if name == "fc2_fwd":  # fp32 residual + dropout epilogue, K = 3072
+        a, w, res = r(M, 4 * C), r(C, 4 * C), torch.randn(M, C, device=dev)
+        bias, out = torch.zeros(C, device=dev), torch.empty(M, C, device=dev)
+        return lambda: K.gemm(K.FWD, K.EPI_RESID, M, C, 4 * C, a, 4 * C, w, 4 * C, out, C, bias=bias, resid=res,
+                              p_drop=0.1, seed=4)
+    if name == "qkv_fwd":
+        a, w, bias = r(M, C), r(3 * C, C), torch.zeros(3 * C, device=dev)
+        out = torch.empty(M, 3 * C, dtype=torch.bfloat16, device=dev)
+        return lambda: K.gemm(K.FWD, K.EPI_BF16, M, 3 * C, C, a, C, w, C, out, 3 * C, bias=bias)
+    if name == "fc2_dgrad":  # GELU-derivative epilogue + fused fc1 bias grad (forward layout against W^T)
+        dy, wt, dg = r(M, C), r(4 * C, C), r(M, 4 * C)
+        out, db = torch.empty(M, 4 * C, dtype=torch.bfloat16, device=dev), torch.zeros(4 * C, device=dev)
+        return lambda: K.gemm(K.FWD, K.EPI_GELU_BWD, M, 4 * C, C, dy, C, wt, C, out, 4 * C, aux=dg, ldaux=4 * C,
+                              dbias=db)
     if name == "attn_fwd":
         qkv, out = r(M, 3 * C), torch.empty(M, C, dtype=torch.bfloat16, device=dev)
         lse = torch.empty(B * H, T, device=dev)

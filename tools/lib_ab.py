@@ -33,12 +33,16 @@ def bind(path, _n=[0]):
     return lib
 
 
+def _sched(lib):
+    return getattr(lib, "sched", 0)
+
+
 def main():
     libs = [bind(p) for p in sys.argv[1:]]
-    # LIB_AB_IMPLS=0,8: gpt2mi_set_gemm_impl per library (the same .so may be listed twice)
+    # LIB_AB_IMPLS=0,2: the GEMM sched argument per library (the same .so may be listed twice)
     impls = [int(v) for v in os.environ.get("LIB_AB_IMPLS", "").split(",") if v]
     for lib, impl in zip(libs, impls):
-        lib.gpt2mi_set_gemm_impl(impl)
+        lib.sched = impl
     Mt, C, Vp = 65536, 768, 50432
     shapes = {"lm_head wgrad": (Vp, C), "qkv wgrad": (3 * C, C), "fc1 wgrad": (4 * C, C), "fc2 wgrad": (C, 4 * C),
               "proj wgrad": (C, C)}
@@ -66,7 +70,7 @@ def main():
         for name, (m, n, A, B, sp, ws) in data.items():
             Cm = torch.zeros(m, n, device=dev)
             rc = lib.gpt2mi_gemm_wgrad(m, n, Mt, A.data_ptr(), m, B.data_ptr(), n, Cm.data_ptr(), n, 0, 1.0, None,
-                                       ws.data_ptr(), ws.numel(), sp, st)
+                                       ws.data_ptr(), ws.numel(), sp, _sched(lib), st)
             assert rc == 0, (i, name, rc)
             outs[(i, name)] = Cm
     torch.cuda.synchronize()
@@ -82,7 +86,7 @@ def main():
             for i, lib in enumerate(libs):
                 Cm = outs[(i, name)]
                 fn = lambda: lib.gpt2mi_gemm_wgrad(m, n, Mt, A.data_ptr(), m, B.data_ptr(), n, Cm.data_ptr(), n, 1,  # noqa
-                                                   1.0, None, ws.data_ptr(), ws.numel(), sp, st)
+                                                   1.0, None, ws.data_ptr(), ws.numel(), sp, _sched(lib), st)
                 fn()
                 s, e = ev(), ev()
                 s.record()
@@ -132,7 +136,7 @@ def gemm_mode(libs, g, st):
             a2 = aux.clone() if aux is not None else None
             assert lib.gpt2mi_gemm(lay, epi, Mt, n, k, A.data_ptr(), k, B.data_ptr(), k if lay == 0 else n, o.data_ptr(),
                                    n, ptr(bias), ptr(resid), ptr(a2), n if aux is not None else 0, 1.0, None, 0, 1, pd,
-                                   5, ptr(db), st) == 0
+                                   5, ptr(db), _sched(lib), st) == 0
             torch.cuda.synchronize()
             if ref is None:
                 ref = (o, a2, db)
@@ -154,7 +158,7 @@ def gemm_mode(libs, g, st):
                     os.environ["GPT2MI_PP_STAGGER"] = str(stag[i])
                 fn = lambda: lib.gpt2mi_gemm(lay, epi, Mt, n, k, A.data_ptr(), k, B.data_ptr(), ldb,  # noqa: E731
                                              out.data_ptr(), n, ptr(bias), ptr(resid), ptr(aux), n if aux is not None else 0,
-                                             1.0, None, 0, 1, pd, 5, ptr(dbs.get(name)), st)
+                                             1.0, None, 0, 1, pd, 5, ptr(dbs.get(name)), _sched(lib), st)
                 assert fn() == 0
                 s, e = ev(), ev()
                 s.record()
