@@ -1,10 +1,13 @@
 #!/usr/bin/env python
 """Derived SQ metrics per kernel from tools/pmc_sq.sh output directories (rocprofv3 --pmc csv; per-launch
 averages, the cold first launch dropped):
-  mfma_busy  = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE * 1024)   share of the 1024 SIMDs' cycles the MFMA
-                                                                    pipe is busy (the counter counts cycles per
-                                                                    SIMD, summed; GRBM_GUI_ACTIVE per XCD, averaged)
-  valu_busy  = SQ_ACTIVE_INST_VALU * 4 / (GRBM_GUI_ACTIVE * 1024)    VALU issue (quad-cycle counter)
+  cyc        = GRBM_GUI_ACTIVE / 8                                  GPU-active cycles of one XCD (the counter is
+                                                                    summed over the 8 XCDs); clock = cyc / duration
+  mfma_busy  = SQ_VALU_MFMA_BUSY_CYCLES / (cyc * 1024)              share of the 1024 SIMDs' cycles the MFMA pipe
+                                                                    is busy (16 cycles per v_mfma_f32_16x16x32_bf16,
+                                                                    summed over SIMDs). Against the 2.4 GHz peak the
+                                                                    kernel reaches mfma_busy * clock / 2.4
+  valu_busy  = SQ_ACTIVE_INST_VALU * 4 / (cyc * 1024)                VALU issue (quad-cycle counter)
   wait_any   = SQ_WAIT_ANY / SQ_WAVE_CYCLES                          share of wave lifetime waiting (any reason)
   wait_inst  = SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES                     ... waiting on s_waitcnt (memory / LDS)
   lds_conf   = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE               LDS bank-conflict cycles per active cycle
@@ -23,6 +26,8 @@ def load(d):
         for r in csv.DictReader(open(f)):
             name = r["Kernel_Name"].replace("(anonymous namespace)::", "")
             agg[(name, r["Counter_Name"])].append(float(r["Counter_Value"]))
+            if r["Counter_Name"] == "GRBM_GUI_ACTIVE":
+                agg[(name, "DURATION_NS")].append(float(r["End_Timestamp"]) - float(r["Start_Timestamp"]))
     out = collections.defaultdict(dict)
     for (k, c), v in agg.items():
         v = v[1:] if len(v) > 1 else v
@@ -39,8 +44,12 @@ def main():
             g = c.get("GRBM_GUI_ACTIVE") or c.get("GRBM_COUNT")
             if not g:
                 continue
-            simd = g * 1024
+            cyc = g / 8
+            simd = cyc * 1024
+            dur = c.get("DURATION_NS", 0)
             row = {
+                "us": dur / 1e3,
+                "clock_ghz": cyc / dur if dur else 0.0,
                 "mfma_busy": c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / simd,
                 "valu_busy": c.get("SQ_ACTIVE_INST_VALU", 0) * 4 / simd,
                 "wait_any": c.get("SQ_WAIT_ANY", 0) / max(1, c.get("SQ_WAVE_CYCLES", 1)),
@@ -51,7 +60,7 @@ def main():
             print("   " + "  ".join(f"{n} {v:.3f}" for n, v in row.items())
                   + f"  | insts mfma {c.get('SQ_INSTS_MFMA', 0):.3g} valu {c.get('SQ_INSTS_VALU', 0):.3g}"
                   + f" lds {c.get('SQ_INSTS_LDS', 0):.3g} salu {c.get('SQ_INSTS_SALU', 0):.3g}"
-                  + f" gui_active {g:.4g} cyc")
+                  + f" xcd_cycles {cyc:.4g}")
 
 
 if __name__ == "__main__":
