@@ -224,8 +224,11 @@ __device__ __forceinline__ void lds_barrier() {
 #endif
 
 // Output tile of item `pid` (GM M-tiles per group share their B tiles in L2).
+#ifndef GPT2MI_PP_GM
+#define GPT2MI_PP_GM 4
+#endif
 __device__ __forceinline__ void tile_of(int pid, int tiles_m, int tiles_n, int& m0, int& n0) {
-  constexpr int GM = 4;
+  constexpr int GM = GPT2MI_PP_GM;
   const int group = pid / (GM * tiles_n);
   const int first_m = group * GM;
   const int gsz = min(tiles_m - first_m, GM);
