@@ -75,8 +75,21 @@ __device__ __forceinline__ void gelu4(f32x4 u, f32x4 m, f32x4& h, f32x4& d) {
 // Epilogue stores are non-temporal (global_store ... nt): the outputs stream to HBM without displacing the
 // operand tiles the other blocks still read from L2 (step A/B: 65.04 -> 64.39 ms of GPU time; qkv / lm_head
 // forward 5-9 % faster in isolation)
+// GEMM_STORE_EXP (A/B builds only, tools/variant_lib.sh): 1 = epilogue stores compiled out (values kept live),
+// 2 = every tile's stores land in rows / columns 0..255 of the output (an L2-resident 128-KB window)
+#ifndef GEMM_STORE_EXP
+#define GEMM_STORE_EXP 0
+#endif
+__device__ __forceinline__ size_t out_idx(int gm, int ld, int gn) {
+  if constexpr (GEMM_STORE_EXP == 2) return (size_t)(gm & 255) * ld + (gn & 255);
+  return (size_t)gm * ld + gn;
+}
 template <typename TE>
 __device__ __forceinline__ void store4(TE* p, f32x4 v) {
+  if constexpr (GEMM_STORE_EXP == 1) {
+    asm volatile("" ::"v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]));
+    return;
+  }
   if constexpr (sizeof(TE) == 2)
     __builtin_nontemporal_store(bf16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])}, reinterpret_cast<bf16x4*>(p));
   else __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
@@ -125,7 +138,7 @@ __device__ __forceinline__ f32x4 epilogue_operand(const GemmParams& P, int gm, i
 template <int EPI, typename TE = bf16, int DROPM = -1>
 __device__ __forceinline__ f32x4 epilogue_apply(const GemmParams& P, int gm, int gn, f32x4 v, f32x4 opnd) {
   const bool drop = DROPM < 0 ? P.thr != 0u : DROPM == 1;
-  const size_t cidx = (size_t)gm * P.ldc + gn;
+  const size_t cidx = out_idx(gm, P.ldc, gn);
   // dropout pair index: element gm*N + gn of the logical [M,N] over 2, mod 2^32 (N and gn are multiples of 4
   // in every kernel: N is a multiple of the tile width, host-checked)
   const uint32_t pidx = (uint32_t)gm * (uint32_t)(P.N >> 1) + (uint32_t)(gn >> 1);
@@ -151,7 +164,7 @@ __device__ __forceinline__ f32x4 epilogue_apply(const GemmParams& P, int gm, int
     f32x4 h, dg, m = {1.f, 1.f, 1.f, 1.f};
     if (drop) m = drop_scale4(P, pidx);
     gelu4(v, m, h, dg);
-    store4<TE>(reinterpret_cast<TE*>(P.aux) + (size_t)gm * P.ldaux + gn, dg);
+    store4<TE>(reinterpret_cast<TE*>(P.aux) + out_idx(gm, P.ldaux, gn), dg);
     store4<TE>(reinterpret_cast<TE*>(P.C) + cidx, h);
   } else if constexpr (EPI == EPI_GELU_BWD) {
     f32x4 o;
@@ -175,6 +188,10 @@ __device__ __forceinline__ f32x4 epilogue_apply(const GemmParams& P, int gm, int
 // Returns the stored bf16 values: the as-stored column sums widen these bits instead of converting again.
 __device__ __forceinline__ bf16x8 store8_bf16(bf16* p, f32x4 a, f32x4 b) {
   const bf16x8 v = {f2bf(a[0]), f2bf(a[1]), f2bf(a[2]), f2bf(a[3]), f2bf(b[0]), f2bf(b[1]), f2bf(b[2]), f2bf(b[3])};
+  if constexpr (GEMM_STORE_EXP == 1) {
+    asm volatile("" ::"v"(__builtin_bit_cast(u32x4, v)));
+    return v;
+  }
   __builtin_nontemporal_store(v, reinterpret_cast<bf16x8*>(p));
   return v;
 }
@@ -187,7 +204,7 @@ __device__ __forceinline__ void epilogue8(const GemmParams& P, int gm, int gn, f
                                           f32x4& r1) {
   static_assert(EPI == EPI_BF16 || EPI == EPI_GELU || EPI == EPI_GELU_BWD, "bf16-output epilogues only");
   const bool drop = DROPM < 0 ? P.thr != 0u : DROPM == 1;
-  bf16* C = reinterpret_cast<bf16*>(P.C) + (size_t)gm * P.ldc + gn;
+  bf16* C = reinterpret_cast<bf16*>(P.C) + out_idx(gm, P.ldc, gn);
   if constexpr (EPI == EPI_BF16) {
     widen8(store8_bf16(C, v0, v1), r0, r1);
   } else if constexpr (EPI == EPI_GELU) {
@@ -199,7 +216,7 @@ __device__ __forceinline__ void epilogue8(const GemmParams& P, int gm, int gn, f
     }
     gelu4(v0, m0, h0, d0);
     gelu4(v1, m1, h1, d1);
-    store8_bf16(reinterpret_cast<bf16*>(P.aux) + (size_t)gm * P.ldaux + gn, d0, d1);
+    store8_bf16(reinterpret_cast<bf16*>(P.aux) + out_idx(gm, P.ldaux, gn), d0, d1);
     store8_bf16(C, h0, h1);
     r0 = h0;
     r1 = h1;

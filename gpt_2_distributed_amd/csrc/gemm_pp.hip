@@ -41,6 +41,11 @@
 namespace {
 
 constexpr int BM = 256, BN = 256, BK = 64;
+// The B fragments of the next K-tile read in phase 4 (kEarly in gemm_pp_kernel; PP_B0_EARLY=0: the round-2 schedule
+// everywhere, for A/B builds)
+#ifndef PP_B0_EARLY
+#define PP_B0_EARLY 1
+#endif
 constexpr int kThreads = 512;
 constexpr int kHalf = 128 * BK * 2;  // 16 KiB
 constexpr int kBuf = 4 * kHalf;      // A_0, A_1, B_0, B_1
@@ -63,37 +68,57 @@ __device__ __forceinline__ int half_map(int ir, int h) {
 }
 
 // One half-tile by LDS-DMA: 16 x 1 KiB instructions, 2 per wave.
-//   TRANS=0 (k-contiguous, src[row][k]): instruction covers image rows 8*ins..+8
-//   TRANS=1 (m-contiguous, src[k][row]): instruction covers k-rows 4*ins..+4
-//   rmax = the operand's last row (TRANS=0) / column (TRANS=1): a partial last tile reads clamped rows / columns
-// 16 zero bytes: the source of every lane of a zero K-tile's DMAs (gemm_pp_kernel, odd K-tile counts)
+//   TRANS=0 (k-contiguous, src[row][k]): instruction covers image rows 8*ins..+8; per-lane 64-bit addresses
+//     (global_load_lds), rows clamped to rmax (the operand's last row) for a partial last tile. (A buffer DMA with a
+//     descriptor per instruction ran these shapes 10-20 % slower: lm_head dgrad 3.64 -> 4.09 ms.)
+//   TRANS=1 (m-contiguous, src[k][row]): instruction covers k-rows 4*ins..+4, by buffer DMA: a lane's source offset
+//     is the same for every instruction, half and K-tile (one VGPR, dma_lane_off) and the instruction's position a
+//     wave-uniform 64-bit base in its descriptor (SALU), so the wgrad keeps no per-lane 64-bit pointers across the
+//     main loop (fits its 256 VGPRs with the phase-4 B reads, kEarly). A partial last tile (extent % 256 != 0, a
+//     multiple of 64) reads past the row's end — the next row's elements, and past the operand's last row up to 192
+//     elements (the caller's allocation covers them, gpt2mi.h); they only feed outputs the epilogue does not store.
+// zero: the zero K-tile of an odd K-tile count (TRANS=0: every lane reads 16 zero bytes; TRANS=1: num_records 0).
+// 16 zero bytes: the source of every lane of a zero K-tile's flat DMAs
 __device__ const u32x4 g_zero16 = {0u, 0u, 0u, 0u};
 
 template <bool TRANS, bool IS_A, bool IL>
+__device__ __forceinline__ uint32_t dma_lane_off(int ld, int lane, int wid) {
+  if constexpr (!TRANS) {
+    return 0u;  // (flat DMA: per-lane addresses)
+  } else {
+    // k = 4 ins + (lane >> 4) with ins = 2 wid + t: k & 3 = lane >> 4 and (k >> 3) & 1 = wid & 1 for both t, so
+    // mc_swz(k) = 2 ((lane >> 4) | (wid & 1) << 2)
+    const int l4 = lane >> 4;
+    const int c = (lane & 15) ^ (2 * (l4 | ((wid & 1) << 2)));
+    return (uint32_t)((l4 * ld + half_map<IL, IS_A>(8 * c, 0)) * (int)sizeof(bf16));
+  }
+}
+__device__ __forceinline__ u32x4 buf_desc_n(const void* base, uint32_t bytes) {
+  const uint64_t a = (uint64_t)(uintptr_t)base;
+  return u32x4{(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)a),
+               (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32) & 0xffffu),
+               (uint32_t)__builtin_amdgcn_readfirstlane(bytes), 0x00020000u};
+}
+template <bool TRANS, bool IS_A, bool IL>
 __device__ __forceinline__ void dma_half(const bf16* __restrict__ src, int ld, int base, int h, int k0, int rmax,
-                                         char* slot, int wid, int lane, bool zero = false) {
+                                         char* slot, int wid, int lane, uint32_t loff, bool zero = false) {
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     const int ins = wid * 2 + t;
-    const bf16* g;
     if constexpr (!TRANS) {
       const int ir = 8 * ins + (lane >> 3);
       const int c = (lane & 7) ^ (ir & 7);
-      g = src + (size_t)min(base + half_map<IL, IS_A>(ir, h), rmax) * ld + k0 + 8 * c;
+      const bf16* g = src + (size_t)min(base + half_map<IL, IS_A>(ir, h), rmax) * ld + k0 + 8 * c;
+      if (zero) {  // branch-free select of the zero source (zero is wave-uniform)
+        const uintptr_t zm = (uintptr_t)0 - (uintptr_t)zero;
+        g = reinterpret_cast<const bf16*>((reinterpret_cast<uintptr_t>(g) & ~zm) |
+                                          (reinterpret_cast<uintptr_t>(&g_zero16) & zm));
+      }
+      lds_dma16(g, slot + ins * 1024);
     } else {
-      const int k = 4 * ins + (lane >> 4);
-      const int c = (lane & 15) ^ mc_swz(k);
-      // a partial last tile (extent % 256 != 0, a multiple of 64) reads past the row's end: the next row's elements,
-      // and past the operand's last row up to 192 elements (the caller's allocation covers them, gpt2mi.h); they
-      // only feed outputs the epilogue does not store
-      g = src + (size_t)(k0 + k) * ld + base + half_map<IL, IS_A>(8 * c, h);
+      const bf16* g = src + (size_t)(k0 + 4 * ins) * ld + base + half_map<IL, IS_A>(0, h);
+      lds_dma16_buf(buf_desc_n(g, zero ? 0u : 0x7fffffffu), loff, 0, slot + ins * 1024);
     }
-    if (zero) {  // branch-free select of the zero source (zero is wave-uniform)
-      const uintptr_t zm = (uintptr_t)0 - (uintptr_t)zero;
-      g = reinterpret_cast<const bf16*>((reinterpret_cast<uintptr_t>(g) & ~zm) |
-                                        (reinterpret_cast<uintptr_t>(&g_zero16) & zm));
-    }
-    lds_dma16(g, slot + ins * 1024);
   }
 }
 
@@ -171,11 +196,22 @@ constexpr int vm_cap(int n) { return n > 63 ? 63 : n; }
 
 // end of a phase's memory segment: retire the half-tile the next phase reads, then the ping-pong
 // MFMA segment between two barriers
+// PP_LGKM_AFTER_BARRIER=0 (A/B builds): no explicit lgkmcnt(0) ahead of the MFMA segment; the compiler's own counted
+// waits retire each fragment read before its first MFMA, and every fragment a memory segment reads is consumed by the
+// MFMA segment that follows it, so all reads still complete before the barrier that ends that segment
+#ifndef PP_LGKM_AFTER_BARRIER
+#define PP_LGKM_AFTER_BARRIER 1
+#endif
+#if PP_LGKM_AFTER_BARRIER
+#define PP_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#else
+#define PP_LGKM0()
+#endif
 #define PP_SYNC_MFMA(ACC, NI, VM)                          \
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM) : "memory"); \
   __builtin_amdgcn_sched_barrier(0);                       \
   __builtin_amdgcn_s_barrier();                            \
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");       \
+  PP_LGKM0()                                               \
   __builtin_amdgcn_sched_barrier(0);                       \
   __builtin_amdgcn_s_setprio(1);                           \
   mfma_quadrant<NI>(ACC, fr);                              \
@@ -190,7 +226,7 @@ constexpr int vm_cap(int n) { return n > 63 ? 63 : n; }
   else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM) : "memory");                       \
   __builtin_amdgcn_sched_barrier(0);                                                  \
   __builtin_amdgcn_s_barrier();                                                       \
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                  \
+  PP_LGKM0()                                                                          \
   __builtin_amdgcn_sched_barrier(0);                                                  \
   __builtin_amdgcn_s_setprio(1);                                                      \
   mfma_quadrant<NI>(ACC, fr);                                                         \
@@ -246,6 +282,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   PP_STAMP(0)
   constexpr bool AIL = MAP & 1, BIL = MAP & 2;  // interleaved half-tile maps (A/B experiments)
   static_assert(!PERSIST || MAP == 0, "the persistent epilogue assumes the contiguous half-tile map");
+  // phase-4 B reads (see ktile): the persistent schedule and the weight gradients (both operands by buffer DMA); the
+  // one-tile-per-block k-contiguous kernels keep the round-2 schedule (their per-lane flat DMA addresses would spill)
+  constexpr bool kB0Early = PP_B0_EARLY && (PERSIST || (A_T && B_T));
   __shared__ __attribute__((aligned(1024))) char smem[kLds];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -300,29 +339,32 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
     rs_b = buf_desc(P.B);
     loff_a = kc_lane_off(P.lda, lane);
     loff_b = kc_lane_off(P.ldb, lane);
+  } else {
+    loff_a = dma_lane_off<A_T, true, AIL>(P.lda, lane, wid);
+    loff_b = dma_lane_off<B_T, false, BIL>(P.ldb, lane, wid);
   }
   auto dma_a_at = [&](int mm0, int t, int h, char* buf) {
     if constexpr (PERSIST)
       dma_half_buf(rs_a, P.lda, mm0 + (h << 7), kofs(t), loff_a, buf + (h ? SA1 : SA0), wid);
     else
-      dma_half<A_T, true, AIL>(P.A, P.lda, mm0, h, kofs(t), P.M - 1, buf + (h ? SA1 : SA0), wid, lane);
+      dma_half<A_T, true, AIL>(P.A, P.lda, mm0, h, kofs(t), P.M - 1, buf + (h ? SA1 : SA0), wid, lane, loff_a);
   };
   auto dma_b_at = [&](int nn0, int t, int h, char* buf) {
     if constexpr (PERSIST)
       dma_half_buf(rs_b, P.ldb, nn0 + (h << 7), kofs(t), loff_b, buf + (h ? SB1 : SB0), wid);
     else
-      dma_half<B_T, false, BIL>(P.B, P.ldb, nn0, h, kofs(t), P.N - 1, buf + (h ? SB1 : SB0), wid, lane);
+      dma_half<B_T, false, BIL>(P.B, P.ldb, nn0, h, kofs(t), P.N - 1, buf + (h ? SB1 : SB0), wid, lane, loff_b);
   };
   auto dma_a = [&](int t, int h, char* buf) { dma_a_at(m0, t, h, buf); };
   auto dma_b = [&](int t, int h, char* buf) { dma_b_at(n0, t, h, buf); };
   // tile 0 of the prologue (zero source when odd; the persistent kernel never is)
   auto dma_a0z = [&](int t, int h, char* buf) {
     if constexpr (PERSIST) dma_a_at(m0, t, h, buf);
-    else dma_half<A_T, true, AIL>(P.A, P.lda, m0, h, kofs(t), P.M - 1, buf + (h ? SA1 : SA0), wid, lane, odd);
+    else dma_half<A_T, true, AIL>(P.A, P.lda, m0, h, kofs(t), P.M - 1, buf + (h ? SA1 : SA0), wid, lane, loff_a, odd);
   };
   auto dma_b0z = [&](int t, int h, char* buf) {
     if constexpr (PERSIST) dma_b_at(n0, t, h, buf);
-    else dma_half<B_T, false, BIL>(P.B, P.ldb, n0, h, kofs(t), P.N - 1, buf + (h ? SB1 : SB0), wid, lane, odd);
+    else dma_half<B_T, false, BIL>(P.B, P.ldb, n0, h, kofs(t), P.N - 1, buf + (h ? SB1 : SB0), wid, lane, loff_b, odd);
   };
   char* buf0 = smem;
   char* buf1 = smem + kBuf;
@@ -334,8 +376,13 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   dma_b0z(0, 0, buf0);
   dma_b0z(0, 1, buf0);
   dma_a0z(0, 1, buf0);
-  dma_a(1, 0, buf1);
-  dma_b(1, 0, buf1);
+  if constexpr (kB0Early) {  // phases -2 / -1 of the schedule below issue B_0 then A_0
+    dma_b(1, 0, buf1);
+    dma_a(1, 0, buf1);
+  } else {
+    dma_a(1, 0, buf1);
+    dma_b(1, 0, buf1);
+  }
   asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A_0(0), B_0(0) landed
   __builtin_amdgcn_s_barrier();
   PP_STAMP(1)
@@ -344,6 +391,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   for (;;) {  // PERSIST: one iteration per output tile (non-persistent: exactly one)
 
   Frags fr;
+  // kB0Early: B_0 of K-tile 0 into slot 0 ahead of its phase 1 (every later K-tile's B_0 is read in the phase 4 before)
+  if constexpr (kB0Early) read_b<B_T, 0>(fr, buf0 + SB0, wc, lane);
   // One K-tile (4 phases): tile tt = t + S, S = 0 / 1 its buffer parity. HN / HN2: tiles tt + 1 / tt + 2 exist. The
   // DMAs for tiles past the end are not issued, and each wait retires what the next phase reads from the real DMAs
   // still outstanding: vmcnt 8,8,8,8 (steady state), 8,8,6,4 (the second-to-last tile), 2,0,0,0 (the last): no
@@ -366,6 +415,30 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
     char* cur = S ? buf1 : buf0;
     char* nxt = S ? buf0 : buf1;
     const int tt = t + S;
+    if constexpr (kB0Early) {
+      // B register slots alternate by parity: B_0 of K-tile tt in slot S, its B_1 in slot 1 - S. Phase 4 reads the NEXT
+      // K-tile's B_0 into slot 1 - S (free once phase 3's MFMAs have read B_1), so no phase reads both operands
+      // fresh: fragment reads per phase 16 / 8 / 16 / 8 for two transposed operands (was 24 / 8 / 16 / 0). The DMAs of
+      // phases 3 / 4 swap (B_0, then A_0 of tile tt + 2) so that phase 3's wait retires B_0 of tt + 1 for phase 4 and
+      // phase 4's wait A_0 of tt + 1 for the next phase 1; the counts are unchanged. WAR: B_0 of tt + 1 is read in
+      // phase 4 and restaged in phase 3 of tt + 1; A_0 of tt is read in phase 1 and restaged in phase 4.
+      // phase 1: quadrant (0,0)
+      read_a<A_T>(fr, cur + SA0, wr, lane);
+      if constexpr (HN) dma_b(tt + 1, 1, nxt);
+      PP_SYNC_MFMA_F(acc[0][0], S, HN ? 8 : 2, first)
+      // phase 2: quadrant (0,1)
+      read_b<B_T, 1 - S>(fr, cur + SB1, wc, lane);
+      if constexpr (HN) dma_a(tt + 1, 1, nxt);
+      PP_SYNC_MFMA_F(acc[0][1], 1 - S, HN ? 8 : 0, first)
+      // phase 3: quadrant (1,1)
+      read_a<A_T>(fr, cur + SA1, wr, lane);
+      if constexpr (HN2) dma_b(tt + 2, 0, cur);
+      PP_SYNC_MFMA(acc[1][1], 1 - S, HN2 ? 8 : (HN ? 6 : 0))
+      // phase 4: quadrant (1,0); B_0 of tt + 1
+      if constexpr (HN) read_b<B_T, 1 - S>(fr, nxt + SB0, wc, lane);
+      if constexpr (HN2) dma_a(tt + 2, 0, cur);
+      PP_SYNC_MFMA(acc[1][0], S, HN2 ? 8 : (HN ? 4 : 0))
+    } else {
     // phase 1: quadrant (0,0)
     read_a<A_T>(fr, cur + SA0, wr, lane);
     read_b<B_T, 0>(fr, cur + SB0, wc, lane);
@@ -382,6 +455,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
     // phase 4: quadrant (1,0) from registers
     if constexpr (HN2) dma_b(tt + 2, 0, cur);
     PP_SYNC_MFMA(acc[1][0], 0, HN2 ? 8 : (HN ? 4 : 0))
+    }
   };
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
@@ -741,8 +815,13 @@ write_image(mi, wr * 64);
     m0 = next_m0;
     n0 = next_n0;
     zero_acc();
-    dma_a(1, 0, buf1);
-    dma_b(1, 0, buf1);
+    if constexpr (kB0Early) {
+      dma_b(1, 0, buf1);
+      dma_a(1, 0, buf1);
+    } else {
+      dma_a(1, 0, buf1);
+      dma_b(1, 0, buf1);
+    }
     // K-tile 0's A_0 / B_0 landed; its B_1 / A_1, the epilogue's kStores stores and K-tile 1's A_0 / B_0 are the
     // younger operations that may stay in flight (see FIRST above)
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(vm_cap(8 + kStores)) : "memory");

@@ -39,12 +39,16 @@ def main():
     fl = 2.0 * M * N * Kd
     kc = lambda: K.gemm(K.FWD, K.EPI_F32, M, N, Kd, a_kc, Kd, b_kc, Kd, c1, N)  # noqa: E731
     mc = lambda: K.gemm_wgrad(M, N, Kd, a_mc, M, b_mc, N, c2, N, accumulate=False, splits=1)  # noqa: E731
-    res = {"kc": [], "mc": []}
+    # one operand transposed (layout 1: A k-contiguous, B m-contiguous)
+    c3 = torch.empty(M, N, device=dev)
+    kb = lambda: K.gemm(1, K.EPI_F32, M, N, Kd, a_kc, Kd, b_mc, N, c3, N)  # noqa: E731
+    res = {"kc": [], "mc": [], "kc_a_mc_b": []}
     for _ in range(4):
         res["kc"].append(timeit(kc))
         res["mc"].append(timeit(mc))
+        res["kc_a_mc_b"].append(timeit(kb))
     torch.cuda.synchronize()
-    err = (c1 - c2).abs().max().item()
+    err = max((c1 - c2).abs().max().item(), (c1 - c3).abs().max().item())
     for k, v in res.items():
         best = min(v)
         print(f"{k}: {' '.join(f'{x:.3f}' for x in v)} ms  best {fl / best / 1e9:.0f} TF/s ({fl / best / 1e9 / 2516.6:.1%})")
