@@ -386,6 +386,7 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const bf16* __
     if (wave_valid && g == 0) delta[(size_t)bh * T + q] = dl[qg];
   }
   const float sl2 = scale * kLog2e;
+  [[maybe_unused]] const uint32_t tk2 = drop_tk2(thr > 0u ? thr : 1u);
   f32x4 dq[2][4];
 #pragma unroll
   for (int qg = 0; qg < 2; ++qg)
@@ -439,14 +440,15 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const bf16* __
         for (int fi = 0; fi < 4; ++fi)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            uint32_t hh = 0;
-            if constexpr (DROP) hh = drop_fin(pre + (uint32_t)(16 * fi + r) * kDropC1, seed_kx(seed));
+            uint32_t km[2] = {~0u, ~0u};  // keep masks of queries q (qg 0) and q ^ 16 (qg 1): one hash
+            if constexpr (DROP)
+              drop_keep_masks(tk2, drop_fin(pre + (uint32_t)(16 * fi + r) * kDropC1, seed_kx(seed)), km[0], km[1]);
 #pragma unroll
             for (int qg = 0; qg < 2; ++qg) {
               float p = __builtin_amdgcn_exp2f(fmaf(s[qg][fi][r], sl2, -lse2[qg]));
               if constexpr (DIAG) p = (k_lo + 16 * fi + 4 * g + r > q_lo + 16 * qg + (lane & 15)) ? 0.f : p;
               float d = dp[qg][fi][r];  // dP' - delta
-              if constexpr (DROP) d = drop_keep16(hh, qg, thr) ? d : -dl[qg];
+              if constexpr (DROP) d = sel_mask(km[qg], d, -dl[qg]);
               s[qg][fi][r] = p * d;
             }
           }
@@ -516,6 +518,7 @@ __global__ __launch_bounds__(64 * kDkdvWaves) __attribute__((amdgpu_waves_per_eu
       }
     }
   const float sl2 = scale * kLog2e;
+  [[maybe_unused]] const uint32_t tk2 = drop_tk2(thr > 0u ? thr : 1u);
   f32x4 dk[2][4], dv[2][4];
 #pragma unroll
   for (int kg = 0; kg < 2; ++kg)
@@ -595,18 +598,19 @@ __global__ __launch_bounds__(64 * kDkdvWaves) __attribute__((amdgpu_waves_per_eu
             const int key = k_lo + 16 * kg + (lane & 15);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              uint32_t hh = 0;  // queries q and q^16 (fl = 0, 1) share one dropout hash
+              uint32_t km[2] = {~0u, ~0u};  // queries q and q^16 (fl = 0, 1) share one dropout hash
               // counter (bh*T + q0 + 4g + 32hq + r) * T + key: a lane base plus (32hq + r) * T + 16kg (uniform)
-              if constexpr (DROP) hh = drop_fin(pre_t + ((uint32_t)(32 * hq + r) * (uint32_t)T + 16u * kg) * kDropC1, seed_kx(seed));
+              if constexpr (DROP)
+                drop_keep_masks(tk2, drop_fin(pre_t + ((uint32_t)(32 * hq + r) * (uint32_t)T + 16u * kg) * kDropC1,
+                                              seed_kx(seed)), km[0], km[1]);
 #pragma unroll
               for (int fl = 0; fl < 2; ++fl) {
                 float p = __builtin_amdgcn_exp2f(fmaf(s[kg][fl][r], sl2, -l4[fl][r]));
                 if constexpr (DIAG) p = (q0 + 16 * (2 * hq + fl) + 4 * g + r < key) ? 0.f : p;
                 float pdv = p, d = dp[kg][fl][r];  // dP' - delta
                 if constexpr (DROP) {
-                  const bool keep = drop_keep16(hh, fl, thr);
-                  pdv = keep ? p : 0.f;
-                  d = keep ? d : -d4[fl][r];
+                  pdv = __uint_as_float(km[fl] & __float_as_uint(p));
+                  d = sel_mask(km[fl], d, -d4[fl][r]);
                 }
                 dp[kg][fl][r] = pdv;  // dropped P (for dV)
                 s[kg][fl][r] = p * d;  // dS

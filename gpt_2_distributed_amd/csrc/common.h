@@ -101,6 +101,19 @@ __host__ __device__ __forceinline__ uint32_t drop_tk2(uint32_t thr) {
 __device__ __forceinline__ uint32_t drop_keep_mask2(uint32_t tk2, uint32_t h) {
   return __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(__builtin_bit_cast(s16x2, tk2), __builtin_bit_cast(s16x2, h)));
 }
+// Both decisions of hash h as 32-bit lane masks (all ones = keep), for selects done as bit operations (v_and_b32 /
+// v_bfi_b32) instead of a compare into an SGPR pair and v_cndmask (whose SGPR read hazard costs an s_nop per pair)
+__device__ __forceinline__ void drop_keep_masks(uint32_t tk2, uint32_t h, uint32_t& m0, uint32_t& m1) {
+  const uint32_t r = drop_keep_mask2(tk2, h);
+  m0 = (uint32_t)__builtin_amdgcn_sbfe((int)r, 15, 1);
+  m1 = (uint32_t)((int)r >> 31);
+}
+// keep ? a : b for a lane mask m from drop_keep_masks
+__device__ __forceinline__ float sel_mask(uint32_t m, float a, float b) {
+  uint32_t r;  // v_bfi_b32: (m & a) | (~m & b) in one instruction (hipcc forms and + and_or from the C expression)
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(__float_as_uint(a)), "v"(__float_as_uint(b)));
+  return __uint_as_float(r);
+}
 // element-indexed form: element i uses half (i & 1) of hash(i >> 1)
 __device__ __forceinline__ bool drop_keep(uint64_t seed, uint64_t idx, uint32_t thr) {
   return drop_keep16(drop_hash(seed32(seed), seed_kx(seed), (uint32_t)(idx >> 1)), (int)(idx & 1), thr);

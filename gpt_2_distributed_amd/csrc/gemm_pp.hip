@@ -561,7 +561,17 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
     csum = f32x4{0.f, 0.f, 0.f, 0.f};
     csum1 = csum;
   }
-  if constexpr (kWide && PERSIST) {
+  if constexpr (GEMM_STORE_EXP == 3 && PERSIST) {
+    // A/B build only: no epilogue at all (the accumulators kept live): the main loop's share of a tile
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) asm volatile("" ::"v"(acc[a][b][i][j]));
+  } else if constexpr (kWide && PERSIST) {
     // four 64-row passes as below; wave wid, half hl reads rows 16it + 2wid + hl (it = 0..3) of the pass's image,
     // columns 8cj..8cj+7 (two 16-B chunks), and stores each output row pair with one 16-B store per lane
 #pragma unroll
