@@ -229,7 +229,7 @@ GPT2MI_EXPORT int gpt2mi_gemm(int layout, int epilogue, int M, int N, int K, con
   GPT2MI_REQUIRE(ldc % 4 == 0 && (ldaux % 4 == 0 || aux == nullptr), "gemm: ldc/ldaux must be multiples of 4");
   GPT2MI_REQUIRE(p_drop <= 0.f || (size_t)M * N < (1ull << 33),
                  "gemm: M*N=%zu exceeds the 32-bit dropout pair index", (size_t)M * N);
-  GemmParams P;
+  GemmParams P{};
   P.A = (const bf16*)A;
   P.B = (const bf16*)B;
   P.C = C;

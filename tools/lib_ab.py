@@ -146,7 +146,8 @@ def gemm_mode(libs, g, st):
             if db is not None and not torch.allclose(db, ref[2], rtol=1e-4, atol=1e-4 * ref[2].abs().max().item()):
                 print(f"MISMATCH lib{i} {name} dbias: {(db - ref[2]).abs().max().item()}", flush=True)
     times = {(i, n): [] for i in range(len(libs)) for n in shapes}
-    stag = [int(v) for v in os.environ.get("LIB_AB_STAGGER", "").split(",") if v]
+    # LIB_AB_STAGGER="0;8000;6000,4": GPT2MI_PP_STAGGER per library ("<ns>[,<groups>]", read per call)
+    stag = [v for v in os.environ.get("LIB_AB_STAGGER", "").split(";") if v]
     ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
     dbs = {name: torch.zeros(v[1], device=dev) for name, v in data.items() if v[6] == K.EPI_GELU_BWD}
     for _ in range(5):
@@ -154,8 +155,8 @@ def gemm_mode(libs, g, st):
             ldb = k if lay == 0 else n
             pd = 0.1 if epi in (K.EPI_GELU, K.EPI_RESID) and "nodrop" not in name else 0.0
             for i, lib in enumerate(libs):
-                if stag:  # LIB_AB_STAGGER=0,12000: GPT2MI_PP_STAGGER per library (read per call)
-                    os.environ["GPT2MI_PP_STAGGER"] = str(stag[i])
+                if stag:
+                    os.environ["GPT2MI_PP_STAGGER"] = stag[i]
                 fn = lambda: lib.gpt2mi_gemm(lay, epi, Mt, n, k, A.data_ptr(), k, B.data_ptr(), ldb,  # noqa: E731
                                              out.data_ptr(), n, ptr(bias), ptr(resid), ptr(aux), n if aux is not None else 0,
                                              1.0, None, 0, 1, pd, 5, ptr(dbs.get(name)), _sched(lib), st)
