@@ -490,7 +490,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   // lanes whose columns lie past N (a partial last column tile; N % 64 == 0, so a lane's 4 / 8 columns are all in or
   // all out) load no operands and store nothing
   const bool col_ok = PERSIST || gnb < P.N;  // (the persistent schedule runs full column tiles only)
-  const bool has_bias = P.bias && EPI != EPI_GELU_BWD && col_ok;
+  // the persistent BF16 epilogue adds its bias in the accumulator layout (bacc below)
+  constexpr bool kBf16Acc = EPI == EPI_BF16 && PERSIST;
+  const bool has_bias = P.bias && EPI != EPI_GELU_BWD && col_ok && !kBf16Acc;
   const f32x4 bias = has_bias ? *reinterpret_cast<const f32x4*>(P.bias + gnb) : f32x4{0.f, 0.f, 0.f, 0.f};
   [[maybe_unused]] f32x4 bias1 = {0.f, 0.f, 0.f, 0.f};
   if constexpr (kWide) {
@@ -501,6 +503,18 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   // vmcnt(0) at the first use of an ordinary load while an LDS-DMA is in flight, which would drain the
   // next tile's DMAs inside the epilogue (the persistent path is only selected for epilogues without
   // other operand loads: BF16, GELU).
+  // kBf16Acc: the bias of the lane's accumulator columns n0 + ni*128 + wc*32 + 16j + 4(l >> 4) + 0..3
+  [[maybe_unused]] f32x4 bacc[2][2];
+  if constexpr (kBf16Acc) {
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        bacc[ni][j] = P.bias ? *reinterpret_cast<const f32x4*>(P.bias + n0 + ni * 128 + wc * 32 + 16 * j + 4 * (lane >> 4))
+                             : f32x4{0.f, 0.f, 0.f, 0.f};
+        asm volatile("" ::"v"(bacc[ni][j][0]), "v"(bacc[ni][j][1]), "v"(bacc[ni][j][2]), "v"(bacc[ni][j][3]));
+      }
+  }
   int next_m0 = 0, next_n0 = 0;
   bool has_next = false;
   if constexpr (PERSIST) {
@@ -571,6 +585,45 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j) asm volatile("" ::"v"(acc[a][b][i][j]));
+  } else if constexpr (kBf16Acc) {
+    // BF16 output: alpha and the bias applied in the accumulator layout, the tile rounded to bf16 into a [128][256]
+    // bf16 image (64 KiB: all of buffer 1, so two 128-row passes of every wave instead of four 64-row fp32 passes; half
+    // the LDS bytes). 8-B chunk c of image row r at c ^ 2(r & 15): conflict-free for the 16-row x 8-B writes and the
+    // 16-B row reads. Then 16 rows per block-wide step: lane (row tid >> 5, 16-B unit tid & 31) loads 8 columns and
+    // stores them with one 16-B store (full 512-B rows per 32 lanes). Bitwise the stores of the fp32-image path.
+    char* img16 = buf1;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+      if (mi) lds_barrier();  // pass 0's reads are done before pass 1 overwrites the image
+      auto put = [&](auto sc) {
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const int r = wr * 64 + 16 * i + (lane & 15);
+              const int c = ni * 32 + wc * 8 + 4 * j + (lane >> 4);
+              f32x4 v = acc[mi][ni][i][j];
+              if constexpr (decltype(sc)::value) v *= alpha;
+              v += bacc[ni][j];
+              const bf16x4 b = {f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+              *reinterpret_cast<bf16x4*>(img16 + r * 512 + 8 * (c ^ (2 * (r & 15)))) = b;
+            }
+      };
+      if (alpha != 1.f) put(std::true_type{});
+      else put(std::false_type{});
+      lds_barrier();
+      const int cu = tid & 31;
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const int r = 16 * it + (tid >> 5);
+        const u32x4 v = *reinterpret_cast<const u32x4*>(img16 + r * 512 + 8 * ((2 * cu) ^ (2 * (r & 15))));
+        bf16* C = reinterpret_cast<bf16*>(P.C) + out_idx(m0 + mi * 128 + r, P.ldc, n0 + 8 * cu);
+        if constexpr (GEMM_STORE_EXP == 1) asm volatile("" ::"v"(v));
+        else __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(C));
+      }
+    }
   } else if constexpr (kWide && PERSIST) {
     // four 64-row passes as below; wave wid, half hl reads rows 16it + 2wid + hl (it = 0..3) of the pass's image,
     // columns 8cj..8cj+7 (two 16-B chunks), and stores each output row pair with one 16-B store per lane
