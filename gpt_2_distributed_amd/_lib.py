@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("GPT2MI_LIB") or os.path.join(_HERE, "libgpt2mi.so")
 
 # the ABI these bindings are written against (include/gpt2mi.h GPT2MI_ABI_VERSION): a stale or foreign
 # library is refused at load instead of being called with the wrong argument lists
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 _c_int, _c_float, _c_size, _c_u64, _p = ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_void_p
 
@@ -65,6 +65,8 @@ _SIGS = {
     "gpt2mi_fsdp_accum": [_p, _c_int, _p, _c_size, _c_int, _p],
     "gpt2mi_gemm_wgrad": [_c_int, _c_int, _c_int, _p, _c_int, _p, _c_int, _p, _c_int, _c_int, _c_float, _p, _p,
                           _c_size, _c_int, _c_int, _p],
+    "gpt2mi_gemm_wgrad_kt": [_c_int, _c_int, _c_int, _p, _c_int, _p, _c_int, _p, _c_int, _c_int, _c_float, _p, _p,
+                             _c_size, _c_int, _c_int, _p],
 }
 _RESTYPES = {"gpt2mi_last_error": ctypes.c_char_p}
 
@@ -177,6 +179,14 @@ def gemm_wgrad(M, N, K, A, lda, B, ldb, C, ldc, accumulate=True, alpha=1.0, alph
                splits=1, sched=SCHED_AUTO):
     ws_n = workspace.numel() if workspace is not None else 0
     _call("gpt2mi_gemm_wgrad", M, N, K, _ptr(A), lda, _ptr(B), ldb, _ptr(C), ldc, int(accumulate), alpha,
+          _ptr(alpha_dev), _ptr(workspace), ws_n, splits, int(sched), _stream())
+
+
+def gemm_wgrad_kt(M, N, K, A, lda, Bt, ldbt, C, ldc, accumulate=True, alpha=1.0, alpha_dev=None, workspace=None,
+                  splits=1, sched=SCHED_AUTO):
+    """gemm_wgrad with B given transposed (Bt [N][K], k-contiguous): the same C[M][N] (+)= alpha A^T B, same bits."""
+    ws_n = workspace.numel() if workspace is not None else 0
+    _call("gpt2mi_gemm_wgrad_kt", M, N, K, _ptr(A), lda, _ptr(Bt), ldbt, _ptr(C), ldc, int(accumulate), alpha,
           _ptr(alpha_dev), _ptr(workspace), ws_n, splits, int(sched), _stream())
 
 

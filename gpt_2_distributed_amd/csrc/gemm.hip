@@ -340,3 +340,43 @@ GPT2MI_EXPORT int gpt2mi_gemm_wgrad(int M, int N, int K, const uint16_t* A, int 
   if (rc) return rc;
   return gpt2mi::splitk_reduce(workspace, splits, (size_t)M * N, C, accumulate, s);
 }
+
+// The same weight gradient with the second operand given TRANSPOSED, k-contiguous: Bt stored [N][K] (X^T, e.g. the
+// final LayerNorm's output transposed once per step). Runs the ping-pong kernel in layout 1 on C^T[N][M] = Bt . A
+// (k-contiguous A operand, m-contiguous B operand: one transposed fragment stream instead of two; the lm_head wgrad
+// split 1.75 -> 1.42 ms, tools/lmwg_ab.py) into split-K slabs, then sums them transposed into C[M][N].
+GPT2MI_EXPORT int gpt2mi_gemm_wgrad_kt(int M, int N, int K, const uint16_t* A, int lda, const uint16_t* Bt, int ldbt,
+                                       float* C, int ldc, int accumulate, float alpha, const float* alpha_dev,
+                                       float* workspace, size_t workspace_floats, int splits, int sched,
+                                       void* stream) {
+  GPT2MI_REQUIRE(M % 64 == 0 && N % 64 == 0 && K % 128 == 0 && M > 0 && N > 0 && K > 0,
+                 "gemm_wgrad_kt: M=%d N=%d must be multiples of 64, K=%d of 128", M, N, K);
+  GPT2MI_REQUIRE(M % 256 == 0, "gemm_wgrad_kt: M=%d must be a multiple of 256 (the transposed operand's full tiles)", M);
+  GPT2MI_REQUIRE(ldc == N, "gemm_wgrad_kt: C must be dense (ldc == N)");
+  GPT2MI_REQUIRE(splits >= 1 && splits <= K / 128, "gemm_wgrad_kt: bad splits %d", splits);
+  GPT2MI_REQUIRE((sched & ~(GPT2MI_SCHED_NO_PERSISTENT | 0xff)) == 0, "gemm_wgrad_kt: bad sched %#x", sched);
+  GPT2MI_REQUIRE(workspace != nullptr, "gemm_wgrad_kt: needs a workspace (splits*M*N floats)");
+  hipStream_t s = (hipStream_t)stream;
+  GemmParams P{};
+  P.A = (const bf16*)Bt;  // C^T[N][M] = Bt[N][K] . A[K][M]
+  P.B = (const bf16*)A;
+  P.M = N; P.N = M; P.K = K; P.lda = ldbt; P.ldb = lda; P.ldc = M;
+  P.alpha = alpha;
+  P.alpha_dev = alpha_dev;
+  const int ktiles = K / 64;
+  int tiles_per = (ktiles + splits - 1) / splits;
+  tiles_per += tiles_per & 1;  // even K-tile counts per split (the ping-pong kernel walks K-tile pairs)
+  P.k_per_split = tiles_per * 64;
+  splits = (K + P.k_per_split - 1) / P.k_per_split;
+  GPT2MI_REQUIRE(workspace_floats >= (size_t)splits * M * N, "gemm_wgrad_kt: workspace of %zu floats < %zu",
+                 workspace_floats, (size_t)splits * M * N);
+  P.C = workspace;
+  const int rc = gpt2mi::gemm_pp_dispatch(1, EPI_SLAB, P, s, splits, 0);
+  if (rc < 0) {
+    gpt2mi::set_error("gemm_wgrad_kt: no kernel for M=%d N=%d K=%d splits=%d", M, N, K, splits);
+    return 22;
+  }
+  if (rc) return rc;
+  return gpt2mi::splitk_reduce_t(workspace, splits, N, M, C, accumulate, s);
+}
+

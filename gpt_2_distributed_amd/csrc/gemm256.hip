@@ -266,6 +266,31 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
 }
 
+// 64 x 64 tile of the slabs per block, summed as splitk_reduce sums (the old value first when accumulating, then the
+// slabs in split order: the same bits), staged through LDS and written transposed; 256-B row segments on both sides
+__global__ __launch_bounds__(256) void splitk_reduce_t_kernel(const float* __restrict__ slab, int splits, int rows,
+                                                              int cols, float* __restrict__ out, int accumulate) {
+  __shared__ float t[64][65];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 4 rows of 64 per pass
+  const size_t plane = (size_t)rows * cols;
+  if (accumulate) {
+#pragma unroll 4
+    for (int i = 0; i < 16; ++i) t[tx][4 * i + ty] = out[(size_t)(c0 + 4 * i + ty) * rows + r0 + tx];
+    __syncthreads();
+  }
+#pragma unroll 4
+  for (int i = 0; i < 16; ++i) {
+    const int r = r0 + 4 * i + ty;
+    float v = accumulate ? t[4 * i + ty][tx] : 0.f;
+    for (int z = 0; z < splits; ++z) v += slab[z * plane + (size_t)r * cols + c0 + tx];
+    t[4 * i + ty][tx] = v;
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int i = 0; i < 16; ++i) out[(size_t)(c0 + 4 * i + ty) * rows + r0 + tx] = t[tx][4 * i + ty];
+}
+
 }  // namespace
 
 namespace gpt2mi {
@@ -286,6 +311,10 @@ int gemm256_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t 
   }
 }
 
+int splitk_reduce_t(const float* slab, int splits, int rows, int cols, float* out, int accumulate, hipStream_t s) {
+  splitk_reduce_t_kernel<<<dim3(cols / 64, rows / 64), 256, 0, s>>>(slab, splits, rows, cols, out, accumulate);
+  return check_launch("splitk_reduce_t");
+}
 int splitk_reduce(const float* slab, int splits, size_t n, float* out, int accumulate, hipStream_t s) {
   splitk_reduce_kernel<<<2048, 256, 0, s>>>(slab, splits, n / 4, out, accumulate);
   return check_launch("splitk_reduce");

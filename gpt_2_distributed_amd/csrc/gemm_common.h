@@ -239,4 +239,6 @@ int gemm256_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t 
 int gemm_pp_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t s, int splits, int map = 0,
                      bool persistent_ok = true);
 int splitk_reduce(const float* slab, int splits, size_t n, float* out, int accumulate, hipStream_t s);
+// out[c][r] (+)= sum_z slab[z][r][c]: slabs [splits][rows][cols] summed in split order and written transposed
+int splitk_reduce_t(const float* slab, int splits, int rows, int cols, float* out, int accumulate, hipStream_t s);
 }

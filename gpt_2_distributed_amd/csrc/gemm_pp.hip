@@ -952,6 +952,8 @@ int gemm_pp_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t 
     return epilogue == EPI_SLAB ? launch<true, true, EPI_SLAB>(P, s, splits)
                                 : epilogue == EPI_F32 ? launch<true, true, EPI_F32>(P, s, 1) : -1;
   }
+  // layout 1 split-K slabs: the weight gradient with its X operand transposed (gpt2mi_gemm_wgrad_kt)
+  if (layout == 1 && epilogue == EPI_SLAB) return P.N % BN == 0 ? launch<false, true, EPI_SLAB>(P, s, splits) : -1;
   if (map > 0 && epilogue == EPI_BF16 && layout <= 1 && P.N % BN == 0) {  // half-tile maps (tools/gemm_probe.py)
     if (layout == 0) {
       if (map == 1) return launch<false, false, EPI_BF16, 1>(P, s, 1);

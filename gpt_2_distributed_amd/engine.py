@@ -151,6 +151,8 @@ class Scratch:
         wshapes = [(3 * C, C), (C, C), (4 * C, C), (C, 4 * C)] + ([(vpad, C)] if head else [])
         need = max((K_wgrad_splits(m, n, M) * m * n if K_wgrad_splits(m, n, M) > 1 else 0)
                    for m, n in wshapes) if C % 64 == 0 and act == BF16 else 0
+        if head and C % 64 == 0 and act == BF16:  # the lm_head's transposed-X wgrad always goes through its slabs
+            need = max(need, K_wgrad_splits(vpad, C, M) * vpad * C)
         self.wgrad_ws = e(max(need, 4), dt=F32)
 
 
@@ -165,6 +167,7 @@ class Workspace(Scratch):
         self.x = e(L + 1, M, C, dt=F32)
         self.blocks: List[BlockActs] = [BlockActs.alloc(cfg, B, T, device, act) for _ in range(L)]
         self.lnf = e(M, C)
+        self.lnf_t = None  # lnf transposed [C][M], formed by the backward for the lm_head wgrad (bf16 only)
         self.mf = e(M, dt=F32)
         self.rf = e(M, dt=F32)
         self.dlogits = e(M, vpad)
@@ -355,6 +358,9 @@ class Engine:
 
     def _gemm_wgrad(self, *a, **kw):
         K.gemm_wgrad(*a, sched=self.gemm_sched, **kw)
+
+    def _gemm_wgrad_kt(self, *a, **kw):
+        K.gemm_wgrad_kt(*a, sched=self.gemm_sched, **kw)
 
     # ---- parameter views ------------------------------------------------------------------------------
     def p(self, name):  # fp32 master view
@@ -792,7 +798,16 @@ class Engine:
                         alpha=gs)
         wte_g = self.layout.padded_view(self.grad, "transformer.wte.weight", Vp)
         with self._probe("lm_head_wgrad"), self._probe("wgrad"):
-            if C % 64 == 0 and act == BF16:
+            if C % 64 == 0 and act == BF16 and M % 128 == 0 and Vp % 256 == 0:
+                # dwte^T = lnf^T . dlogits with lnf transposed once (0.1 GB at cfg 2): one transposed GEMM operand
+                # instead of two (gpt2mi_gemm_wgrad_kt; lm_head wgrad ~18 % faster, the same bits)
+                if ws.lnf_t is None:
+                    ws.lnf_t = torch.empty(C, M, dtype=act, device=ws.lnf.device)
+                K.transpose_bf16(ws.lnf, ws.lnf_t, M, C, C, M)
+                self._gemm_wgrad_kt(Vp, C, M, ws.dlogits, Vp, ws.lnf_t, M, wte_g, C, accumulate=not self._grad_fresh,
+                                    alpha_dev=alpha_dev, alpha=gs, workspace=ws.wgrad_ws,
+                                    splits=K_wgrad_splits(Vp, C, M))
+            elif C % 64 == 0 and act == BF16:
                 self._gemm_wgrad(Vp, C, M, ws.dlogits, Vp, ws.lnf, C, wte_g, C, accumulate=not self._grad_fresh,
                              alpha_dev=alpha_dev, alpha=gs, workspace=ws.wgrad_ws, splits=K_wgrad_splits(Vp, C, M))
             else:

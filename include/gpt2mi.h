@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GPT2MI_ABI_VERSION 8
+#define GPT2MI_ABI_VERSION 9
 
 const char* gpt2mi_last_error(void);
 int gpt2mi_abi_version(void); /* returns GPT2MI_ABI_VERSION of the built library */
@@ -95,6 +95,14 @@ int gpt2mi_gemm(int layout, int epilogue, int M, int N, int K, const uint16_t* A
 int gpt2mi_gemm_wgrad(int M, int N, int K, const uint16_t* A, int lda, const uint16_t* B, int ldb, float* C, int ldc,
                       int accumulate, float alpha, const float* alpha_dev, float* workspace, size_t workspace_floats,
                       int splits, int sched, void* stream);
+/* The same weight gradient with B given transposed, k-contiguous: Bt stored [N][K] (X^T; train_gpt2_distributed.py:412,
+ * the tied lm_head's wgrad against the final LayerNorm output transposed once per step). Computes C^T = Bt . A on the
+ * ping-pong kernel (one transposed operand instead of two) into split-K slabs (workspace >= splits*M*N floats,
+ * required) and sums them, transposed, into C (fixed order: the same bits as gpt2mi_gemm_wgrad). M multiple of 256,
+ * N of 64, K of 128; ldc == N. ABI v9. */
+int gpt2mi_gemm_wgrad_kt(int M, int N, int K, const uint16_t* A, int lda, const uint16_t* Bt, int ldbt, float* C,
+                         int ldc, int accumulate, float alpha, const float* alpha_dev, float* workspace,
+                         size_t workspace_floats, int splits, int sched, void* stream);
 
 /* K4-K8: causal flash attention, head_dim 64 — model.py:124-155. q/k/v read from qkv [B*T, 3C];
  * out [B*T, C] head-merged; lse [B*H, T] (natural log of the 1/sqrt(D)-scaled scores). */

@@ -675,3 +675,29 @@ def test_gemm_wgrad_edge_tiles_vs_fp64(m, n, tokens, splits):
     assert rel_err(C1[rows].double().cpu(), ref.cpu()) < 1e-5
     assert rel_err(C[rows].double().cpu(), 2 * ref.cpu()) < 1e-5
     assert not torch.isnan(C).any()
+
+
+@pytest.mark.parametrize("m,n,tokens,splits", [(512, 192, 1024, 3), (768, 1600, 2048, 2), (50432, 768, 1024, 3),
+                                               (256, 64, 256, 1)])
+def test_gemm_wgrad_kt_same_bits_as_wgrad(m, n, tokens, splits):
+    """gpt2mi_gemm_wgrad_kt (the X operand given transposed: the tied lm_head's wgrad against lnf^T) against
+    gpt2mi_gemm_wgrad on the same operands — the same split-K slabs summed in the same order, so the same bits — with
+    write (lazy-zeroed arena) and accumulate, alpha and a device alpha; and against float64 on sampled rows."""
+    g = torch.Generator().manual_seed(m + n + tokens + splits)
+    A = _tail(bf(torch.randn(tokens, m, generator=g) * 0.1))
+    B = _tail(bf(torch.randn(tokens, n, generator=g)))  # (gemm_wgrad's partial-tile reads past the last row)
+    Bt = B.t().contiguous()
+    ad = torch.tensor([0.75], device=dev)
+    ws = torch.empty(max(4, splits * m * n), device=dev)
+    C0 = torch.randn(m, n, generator=g).to(dev)
+    for acc in (False, True):
+        C1, C2 = C0.clone(), C0.clone()
+        L().gemm_wgrad(m, n, tokens, A, m, B, n, C1, n, accumulate=acc, alpha=0.5, alpha_dev=ad, workspace=ws,
+                       splits=splits)
+        L().gemm_wgrad_kt(m, n, tokens, A, m, Bt, tokens, C2, n, accumulate=acc, alpha=0.5, alpha_dev=ad,
+                          workspace=ws, splits=splits)
+        torch.cuda.synchronize()
+        assert torch.equal(C1, C2), (acc, (C1 - C2).abs().max().item())
+        rows = torch.cat([torch.arange(0, m, max(1, m // 24), device=dev), torch.arange(m - 8, m, device=dev)])
+        ref = 0.375 * (A[:, rows].double().t() @ B.double()) + (C0[rows].double() if acc else 0)
+        assert rel_err(C2[rows].double().cpu(), ref.cpu()) < 1e-5
