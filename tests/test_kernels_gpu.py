@@ -701,3 +701,41 @@ def test_gemm_wgrad_kt_same_bits_as_wgrad(m, n, tokens, splits):
         rows = torch.cat([torch.arange(0, m, max(1, m // 24), device=dev), torch.arange(m - 8, m, device=dev)])
         ref = 0.375 * (A[:, rows].double().t() @ B.double()) + (C0[rows].double() if acc else 0)
         assert rel_err(C2[rows].double().cpu(), ref.cpu()) < 1e-5
+
+
+@pytest.mark.parametrize("m,n", [(50432, 768), (2304, 768), (768, 3072)])
+def test_wgrad_full_size_vs_fp64(m, n):
+    """The step's weight gradients at BASELINE cfg 2's full size (65 536 tokens, the split-K factor the engine picks)
+    against float64 on sampled output rows — the tied lm_head (also through gpt2mi_gemm_wgrad_kt, its transposed-X
+    form), qkv and fc2 — not only against each other."""
+    tokens = 65536
+    sp = L().wgrad_splits(m, n, tokens)
+    g = torch.Generator(device=dev).manual_seed(m + n)
+    A = (torch.randn(tokens, m, device=dev, generator=g) * 0.05).to(torch.bfloat16)
+    B = torch.randn(tokens, n, device=dev, generator=g).to(torch.bfloat16)
+    ws = torch.empty(max(4, sp * m * n), device=dev)
+    C = torch.empty(m, n, device=dev)
+    L().gemm_wgrad(m, n, tokens, A, m, B, n, C, n, accumulate=False, alpha=0.5, workspace=ws, splits=sp)
+    rows = torch.cat([torch.arange(0, m, max(1, m // 16), device=dev), torch.arange(m - 4, m, device=dev)])
+    ref = 0.5 * (A[:, rows].double().t() @ B.double())
+    assert rel_err(C[rows].double().cpu(), ref.cpu()) < 1e-5
+    if m % 256 == 0:
+        Bt = B.t().contiguous()
+        C2 = torch.empty(m, n, device=dev)
+        L().gemm_wgrad_kt(m, n, tokens, A, m, Bt, tokens, C2, n, accumulate=False, alpha=0.5, workspace=ws, splits=sp)
+        torch.cuda.synchronize()
+        assert torch.equal(C, C2)
+
+
+def test_lm_head_dgrad_full_size_vs_fp64():
+    """dlnf = dlogits . wte at cfg 2's full size (65 536 x 768 over K = 50 432, the forward layout against the
+    transposed wte shadow) against float64 on sampled rows."""
+    M, N, Kd = 65536, 768, 50432
+    g = torch.Generator(device=dev).manual_seed(5)
+    dl = (torch.randn(M, Kd, device=dev, generator=g) * 0.01).to(torch.bfloat16)
+    wt = torch.randn(N, Kd, device=dev, generator=g).to(torch.bfloat16)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    L().gemm(0, L().EPI_BF16, M, N, Kd, dl, Kd, wt, Kd, out, N)
+    rows = torch.arange(0, M, M // 32, device=dev)
+    ref = dl[rows].double() @ wt.double().t()
+    assert rel_err(out[rows].double().cpu(), ref.cpu()) < 8e-3
