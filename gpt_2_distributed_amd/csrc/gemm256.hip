@@ -267,28 +267,48 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 }
 
 // 64 x 64 tile of the slabs per block, summed as splitk_reduce sums (the old value first when accumulating, then the
-// slabs in split order: the same bits), staged through LDS and written transposed; 256-B row segments on both sides
+// slabs in split order: the same bits), staged through LDS and written transposed: 16-B loads and stores, 16 lanes per
+// 256-B row segment on both sides
 __global__ __launch_bounds__(256) void splitk_reduce_t_kernel(const float* __restrict__ slab, int splits, int rows,
                                                               int cols, float* __restrict__ out, int accumulate) {
   __shared__ float t[64][65];
   const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 4 rows of 64 per pass
+  const int q = threadIdx.x & 15, p = threadIdx.x >> 4;  // 16 lanes x 4 floats per 64-float segment, 16 segments / pass
   const size_t plane = (size_t)rows * cols;
-  if (accumulate) {
-#pragma unroll 4
-    for (int i = 0; i < 16; ++i) t[tx][4 * i + ty] = out[(size_t)(c0 + 4 * i + ty) * rows + r0 + tx];
+  if (accumulate) {  // t[r][c] = out[c][r]
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = 16 * i + p;
+      const f32x4 v = *reinterpret_cast<const f32x4*>(out + (size_t)(c0 + c) * rows + r0 + 4 * q);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) t[4 * q + e][c] = v[e];
+    }
     __syncthreads();
   }
-#pragma unroll 4
-  for (int i = 0; i < 16; ++i) {
-    const int r = r0 + 4 * i + ty;
-    float v = accumulate ? t[4 * i + ty][tx] : 0.f;
-    for (int z = 0; z < splits; ++z) v += slab[z * plane + (size_t)r * cols + c0 + tx];
-    t[4 * i + ty][tx] = v;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = 16 * i + p;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (accumulate) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = t[r][4 * q + e];
+    }
+    const float* src = slab + (size_t)(r0 + r) * cols + c0 + 4 * q;
+    for (int z = 0; z < splits; ++z) {
+      const f32x4 w = *reinterpret_cast<const f32x4*>(src + z * plane);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] += w[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) t[r][4 * q + e] = v[e];  // (the lane's own elements: read above, by it alone)
   }
   __syncthreads();
-#pragma unroll 4
-  for (int i = 0; i < 16; ++i) out[(size_t)(c0 + 4 * i + ty) * rows + r0 + tx] = t[tx][4 * i + ty];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = 16 * i + p;
+    const f32x4 v = {t[4 * q][c], t[4 * q + 1][c], t[4 * q + 2][c], t[4 * q + 3][c]};
+    *reinterpret_cast<f32x4*>(out + (size_t)(c0 + c) * rows + r0 + 4 * q) = v;
+  }
 }
 
 }  // namespace

@@ -27,6 +27,16 @@ def make(name):
     if name == "lm_head_dgrad":  # forward layout against the transposed wte shadow
         dl, wt, out = r(M, Vp), r(C, Vp), torch.empty(M, C, dtype=torch.bfloat16, device=dev)
         return lambda: K.gemm(K.FWD, K.EPI_BF16, M, C, Vp, dl, Vp, wt, Vp, out, C)
+    if name == "lm_head_wgrad_kt":  # the step's form: lnf transposed once, gpt2mi_gemm_wgrad_kt
+        dl, x, g = r(M, Vp), r(M, C), torch.zeros(Vp, C, device=dev)
+        xt = torch.empty(C, M, dtype=torch.bfloat16, device=dev)
+        sp = K.wgrad_splits(Vp, C, M)
+        ws = torch.empty(sp * Vp * C, device=dev)
+
+        def run():
+            K.transpose_bf16(x, xt, M, C, C, M)
+            K.gemm_wgrad_kt(Vp, C, M, dl, Vp, xt, M, g, C, workspace=ws, splits=sp)
+        return run
     if name == "lm_head_wgrad":
         dl, x, g = r(M, Vp), r(M, C), torch.zeros(Vp, C, device=dev)
         sp = K.wgrad_splits(Vp, C, M)
