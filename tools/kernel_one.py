@@ -27,7 +27,7 @@ def make(name):
     if name == "lm_head_dgrad":  # forward layout against the transposed wte shadow
         dl, wt, out = r(M, Vp), r(C, Vp), torch.empty(M, C, dtype=torch.bfloat16, device=dev)
         return lambda: K.gemm(K.FWD, K.EPI_BF16, M, C, Vp, dl, Vp, wt, Vp, out, C)
-    if name == "lm_head_wgrad_kt":  # the step's form: lnf transposed once, gpt2mi_gemm_wgrad_kt
+    if name in ("lm_head_wgrad", "lm_head_wgrad_kt"):  # the step's form: lnf transposed once, gpt2mi_gemm_wgrad_kt
         dl, x, g = r(M, Vp), r(M, C), torch.zeros(Vp, C, device=dev)
         xt = torch.empty(C, M, dtype=torch.bfloat16, device=dev)
         sp = K.wgrad_splits(Vp, C, M)
@@ -37,7 +37,7 @@ def make(name):
             K.transpose_bf16(x, xt, M, C, C, M)
             K.gemm_wgrad_kt(Vp, C, M, dl, Vp, xt, M, g, C, workspace=ws, splits=sp)
         return run
-    if name == "lm_head_wgrad":
+    if name == "lm_head_wgrad_old":
         dl, x, g = r(M, Vp), r(M, C), torch.zeros(Vp, C, device=dev)
         sp = K.wgrad_splits(Vp, C, M)
         ws = torch.empty(sp * Vp * C, device=dev)
@@ -83,10 +83,16 @@ def make(name):
         ops = {(m, n): (r(M, m), r(M, n), torch.zeros(m, n, device=dev)) for m, n in set(shapes)}
         ws = torch.empty(max(K.wgrad_splits(m, n, M) * m * n for m, n in shapes), device=dev)
 
-        def run():
+        xt = torch.empty(C, M, dtype=torch.bfloat16, device=dev)
+
+        def run():  # the lm_head as the step runs it: lnf transposed, gpt2mi_gemm_wgrad_kt
             for m, n in shapes:
                 a, x, g = ops[(m, n)]
-                K.gemm_wgrad(m, n, M, a, m, x, n, g, n, workspace=ws, splits=K.wgrad_splits(m, n, M))
+                if m == Vp:
+                    K.transpose_bf16(x, xt, M, C, C, M)
+                    K.gemm_wgrad_kt(m, n, M, a, m, xt, M, g, n, workspace=ws, splits=K.wgrad_splits(m, n, M))
+                else:
+                    K.gemm_wgrad(m, n, M, a, m, x, n, g, n, workspace=ws, splits=K.wgrad_splits(m, n, M))
         return run
     raise SystemExit(f"unknown kernel {name}")
 

@@ -25,8 +25,8 @@ ALGO = {  # algorithmic bytes per launch (operands read once, outputs written on
               + 2 * 65536 * (50432 + 768) + 8 * 50432 * 768) // 49,
 }
 # kernels whose counters make up one probed launch (the wgrad probe = split-K GEMM + slab reduction)
-KERNEL_KEY = {"attn_fwd": ("attn_fwd",), "lm_head_wgrad": ("gemm_pp", "splitk_reduce"),
-              "wgrad": ("gemm_pp", "splitk_reduce")}
+KERNEL_KEY = {"attn_fwd": ("attn_fwd",), "lm_head_wgrad": ("gemm_pp", "splitk_reduce", "transpose_bf16"),
+              "wgrad": ("gemm_pp", "splitk_reduce")}  # (the lm_head's one lnf transpose per 49 launches: 0.4 %)
 # launches of one repetition of a family probe (the per-launch figure averages the last repetition's launches)
 FAMILY = {"wgrad": 49}
 
