@@ -33,6 +33,9 @@ constexpr int BKV = 64;  // keys per K/V tile in fwd / dQ
 #ifndef ATTN_FWD_OCC
 #define ATTN_FWD_OCC 3  // forward waves per SIMD the register budget is cut for (launch bounds)
 #endif
+#ifndef ATTN_FWD_LMAX
+#define ATTN_FWD_LMAX 1  // forward rescale test on each lane's own scores (0: cross-lane max every tile, A/B builds)
+#endif
 #ifndef ATTN_DKDV_WAVES
 #define ATTN_DKDV_WAVES 4
 #endif
@@ -78,6 +81,14 @@ __device__ __forceinline__ float xor_sum(float v) {
   v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
   auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+// max of a lane's 16 scores as a v_max3 tree: 8 instructions (5 + 2 + 1)
+__device__ __forceinline__ float max3f(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
+__device__ __forceinline__ float max16(const f32x4 (&s)[4]) {
+  const float t0 = max3f(s[0][0], s[0][1], s[0][2]), t1 = max3f(s[0][3], s[1][0], s[1][1]);
+  const float t2 = max3f(s[1][2], s[1][3], s[2][0]), t3 = max3f(s[2][1], s[2][2], s[2][3]);
+  const float t4 = max3f(s[3][0], s[3][1], s[3][2]);
+  return fmaxf(max3f(t0, t1, t2), max3f(t3, t4, s[3][3]));
 }
 // Sum over the 16 lanes of a DPP row (lanes with the same l >> 4): every lane gets the row total.
 __device__ __forceinline__ float row16_sum(float x) {
@@ -264,16 +275,25 @@ __global__ __launch_bounds__(kThreads, ATTN_FWD_OCC) void attn_fwd_kernel(const 
       }
 #pragma unroll
       for (int qg = 0; qg < 2; ++qg) {
+        // thresholded rescale (defer-max): keep the running max unless some row of the wave grew by
+        // more than kRescaleThr (log2 units); P then stays below 2^kRescaleThr. Wave-uniform decision,
+        // taken before this tile is exponentiated, so O, l and P all see the same max.
+#if ATTN_FWD_LMAX
+        // The test needs no max across the 4 lanes of a query: they share m, and x -> x * sl2 is monotonic, so
+        // "every lane's own 16 keys pass" is the same decision as "every query's 64 keys pass". The cross-lane
+        // max is formed only when a rescale is taken (same cand, same bits as the all-lanes form).
+        const float lmax = max16(s[qg]);
+        if (!__all(lmax * sl2 <= m[qg] + kRescaleThr)) {
+          const float cand = xor_max(lmax) * sl2;
+#else
         float tmax = -INFINITY;  // max of the raw scores (scale > 0)
 #pragma unroll
         for (int fi = 0; fi < 4; ++fi)
           tmax = fmaxf(tmax, fmaxf(fmaxf(s[qg][fi][0], s[qg][fi][1]), fmaxf(s[qg][fi][2], s[qg][fi][3])));
         tmax = xor_max(tmax);
-        // thresholded rescale (defer-max): keep the running max unless some row of the wave grew by
-        // more than kRescaleThr (log2 units); P then stays below 2^kRescaleThr. Wave-uniform decision,
-        // taken before this tile is exponentiated, so O, l and P all see the same max.
         const float cand = tmax * sl2;
         if (!__all(cand <= m[qg] + kRescaleThr)) {
+#endif
           const float mn = fmaxf(m[qg], cand);  // finite: tile 0 holds key 0, visible to every query
           const float corr = __builtin_amdgcn_exp2f(m[qg] - mn);
 #pragma unroll
