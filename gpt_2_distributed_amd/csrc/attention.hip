@@ -36,6 +36,9 @@ constexpr int BKV = 64;  // keys per K/V tile in fwd / dQ
 #ifndef ATTN_FWD_LMAX
 #define ATTN_FWD_LMAX 1  // forward rescale test on each lane's own scores (0: cross-lane max every tile, A/B builds)
 #endif
+#ifndef ATTN_DKDV_SB
+#define ATTN_DKDV_SB 1  // dK/dV: scheduling barrier between the two 32-query halves of a tile (0: A/B builds)
+#endif
 #ifndef ATTN_DKDV_WAVES
 #define ATTN_DKDV_WAVES 4
 #endif
@@ -651,7 +654,9 @@ __global__ __launch_bounds__(64 * kDkdvWaves) __attribute__((amdgpu_waves_per_eu
           dk[0][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qt, s0, dk[0][fd], 0, 0, 0);
           dk[1][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qt, s1, dk[1][fd], 0, 0, 0);
         }
+#if ATTN_DKDV_SB
         __builtin_amdgcn_sched_barrier(0);
+#endif
       }
     }
     if (i + 1 < nqt) sstore(smem + (cur ^ 1) * kStage);
