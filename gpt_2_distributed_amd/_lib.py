@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("GPT2MI_LIB") or os.path.join(_HERE, "libgpt2mi.so")
 
 # the ABI these bindings are written against (include/gpt2mi.h GPT2MI_ABI_VERSION): a stale or foreign
 # library is refused at load instead of being called with the wrong argument lists
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 _c_int, _c_float, _c_size, _c_u64, _p = ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_void_p
 
@@ -135,6 +135,8 @@ FWD, DGRAD, WGRAD = 0, 1, 2
 # GEMM schedule per call (gpt2mi.h GPT2MI_SCHED_*): auto, or the flag that keeps the persistent schedule off while
 # RCCL kernels may share the CUs; the low byte picks a kernel for A/B experiments and kernel-equivalence tests
 SCHED_AUTO, SCHED_NO_PERSISTENT = 0, 0x100
+# gemm_wgrad / gemm_wgrad_kt: split-K partial sums rounded to bf16 slabs (gpt2mi.h GPT2MI_SCHED_BF16_SLABS)
+SCHED_BF16_SLABS = 0x200
 
 
 def embed_fwd(idx, wte, wpe, x, B, T, C, p=0.0, seed=0, T_valid=None):

@@ -299,9 +299,10 @@ GPT2MI_EXPORT int gpt2mi_gemm_wgrad(int M, int N, int K, const uint16_t* A, int 
                  "gemm_wgrad: M=%d N=%d K=%d must be multiples of 64", M, N, K);
   GPT2MI_REQUIRE(ldc == N, "gemm_wgrad: C must be dense (ldc == N)");
   GPT2MI_REQUIRE(splits >= 1 && splits <= K / 64, "gemm_wgrad: bad splits %d", splits);
-  GPT2MI_REQUIRE((sched & ~(GPT2MI_SCHED_NO_PERSISTENT | 0xff)) == 0 && (sched & 0xff) <= 8, "gemm_wgrad: bad sched %#x",
-                 sched);
+  GPT2MI_REQUIRE((sched & ~(GPT2MI_SCHED_NO_PERSISTENT | GPT2MI_SCHED_BF16_SLABS | 0xff)) == 0 && (sched & 0xff) <= 8,
+                 "gemm_wgrad: bad sched %#x", sched);
   const int impl = sched & 0xff;  // 2: the 2-stage 256x256 kernel (A/B); 0 / 8: the ping-pong kernel
+  const bool slab16 = (sched & GPT2MI_SCHED_BF16_SLABS) != 0;
   hipStream_t s = (hipStream_t)stream;
   GemmParams P{};
   P.A = (const bf16*)A;
@@ -335,9 +336,12 @@ GPT2MI_EXPORT int gpt2mi_gemm_wgrad(int M, int N, int K, const uint16_t* A, int 
                  "gemm_wgrad: workspace of %zu floats < splits*M*N = %zu", workspace_floats, (size_t)splits * M * N);
   P.C = workspace;
   P.accumulate = 0;
-  int rc = pp ? gpt2mi::gemm_pp_dispatch(2, EPI_SLAB, P, s, splits, 0) : -1;
+  // bf16 slabs on the ping-pong kernel only (the 2-stage fallback writes fp32 ones)
+  int rc = pp ? gpt2mi::gemm_pp_dispatch(2, slab16 ? EPI_SLAB16 : EPI_SLAB, P, s, splits, 0) : -1;
+  const bool b16 = slab16 && rc >= 0;
   if (rc < 0) rc = gpt2mi::gemm256_dispatch(2, EPI_SLAB, P, s, splits);
   if (rc) return rc;
+  if (b16) return gpt2mi::splitk_reduce16((const bf16*)workspace, splits, (size_t)M * N, C, accumulate, s);
   return gpt2mi::splitk_reduce(workspace, splits, (size_t)M * N, C, accumulate, s);
 }
 
@@ -354,7 +358,9 @@ GPT2MI_EXPORT int gpt2mi_gemm_wgrad_kt(int M, int N, int K, const uint16_t* A, i
   GPT2MI_REQUIRE(M % 256 == 0, "gemm_wgrad_kt: M=%d must be a multiple of 256 (the transposed operand's full tiles)", M);
   GPT2MI_REQUIRE(ldc == N, "gemm_wgrad_kt: C must be dense (ldc == N)");
   GPT2MI_REQUIRE(splits >= 1 && splits <= K / 128, "gemm_wgrad_kt: bad splits %d", splits);
-  GPT2MI_REQUIRE((sched & ~(GPT2MI_SCHED_NO_PERSISTENT | 0xff)) == 0, "gemm_wgrad_kt: bad sched %#x", sched);
+  GPT2MI_REQUIRE((sched & ~(GPT2MI_SCHED_NO_PERSISTENT | GPT2MI_SCHED_BF16_SLABS | 0xff)) == 0,
+                 "gemm_wgrad_kt: bad sched %#x", sched);
+  const bool slab16 = (sched & GPT2MI_SCHED_BF16_SLABS) != 0;
   GPT2MI_REQUIRE(workspace != nullptr, "gemm_wgrad_kt: needs a workspace (splits*M*N floats)");
   hipStream_t s = (hipStream_t)stream;
   GemmParams P{};
@@ -371,12 +377,15 @@ GPT2MI_EXPORT int gpt2mi_gemm_wgrad_kt(int M, int N, int K, const uint16_t* A, i
   GPT2MI_REQUIRE(workspace_floats >= (size_t)splits * M * N, "gemm_wgrad_kt: workspace of %zu floats < %zu",
                  workspace_floats, (size_t)splits * M * N);
   P.C = workspace;
-  const int rc = gpt2mi::gemm_pp_dispatch(1, EPI_SLAB, P, s, splits, 0);
+  // one split: an fp32 slab, as gpt2mi_gemm_wgrad writes one split straight into C (the same bits)
+  const bool b16 = slab16 && splits > 1;
+  const int rc = gpt2mi::gemm_pp_dispatch(1, b16 ? EPI_SLAB16 : EPI_SLAB, P, s, splits, 0);
   if (rc < 0) {
     gpt2mi::set_error("gemm_wgrad_kt: no kernel for M=%d N=%d K=%d splits=%d", M, N, K, splits);
     return 22;
   }
   if (rc) return rc;
+  if (b16) return gpt2mi::splitk_reduce16_t((const bf16*)workspace, splits, N, M, C, accumulate, s);
   return gpt2mi::splitk_reduce_t(workspace, splits, N, M, C, accumulate, s);
 }
 

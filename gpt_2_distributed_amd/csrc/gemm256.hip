@@ -266,10 +266,35 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
 }
 
+// bf16 slabs (GPT2MI_SCHED_BF16_SLABS): 8 elements per thread (one 16-B load per slab), each widened to fp32 and added
+// in the order above (the old value first when accumulating, then the slabs in split order)
+__global__ __launch_bounds__(256) void splitk_reduce16_kernel(const bf16* __restrict__ slab, int splits, size_t n8,
+                                                              float* __restrict__ out, int accumulate) {
+  for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < n8; i += (size_t)gridDim.x * 256) {
+    f32x4* o = reinterpret_cast<f32x4*>(out) + 2 * i;
+    f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0;
+    if (accumulate) {
+      s0 = o[0];
+      s1 = o[1];
+    }
+    for (int z = 0; z < splits; ++z) {
+      const bf16x8 v = reinterpret_cast<const bf16x8*>(slab + (size_t)z * n8 * 8)[i];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        s0[e] += bf2f(v[e]);
+        s1[e] += bf2f(v[4 + e]);
+      }
+    }
+    o[0] = s0;
+    o[1] = s1;
+  }
+}
+
 // 64 x 64 tile of the slabs per block, summed as splitk_reduce sums (the old value first when accumulating, then the
 // slabs in split order: the same bits), staged through LDS and written transposed: 16-B loads and stores, 16 lanes per
 // 256-B row segment on both sides
-__global__ __launch_bounds__(256) void splitk_reduce_t_kernel(const float* __restrict__ slab, int splits, int rows,
+template <typename TS>  // slab element: float, or bf16 (GPT2MI_SCHED_BF16_SLABS)
+__global__ __launch_bounds__(256) void splitk_reduce_t_kernel(const TS* __restrict__ slab, int splits, int rows,
                                                               int cols, float* __restrict__ out, int accumulate) {
   __shared__ float t[64][65];
   const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
@@ -293,9 +318,9 @@ __global__ __launch_bounds__(256) void splitk_reduce_t_kernel(const float* __res
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = t[r][4 * q + e];
     }
-    const float* src = slab + (size_t)(r0 + r) * cols + c0 + 4 * q;
+    const TS* src = slab + (size_t)(r0 + r) * cols + c0 + 4 * q;
     for (int z = 0; z < splits; ++z) {
-      const f32x4 w = *reinterpret_cast<const f32x4*>(src + z * plane);
+      const f32x4 w = load4<TS>(src + z * plane);
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] += w[e];
     }
@@ -332,8 +357,16 @@ int gemm256_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t 
 }
 
 int splitk_reduce_t(const float* slab, int splits, int rows, int cols, float* out, int accumulate, hipStream_t s) {
-  splitk_reduce_t_kernel<<<dim3(cols / 64, rows / 64), 256, 0, s>>>(slab, splits, rows, cols, out, accumulate);
+  splitk_reduce_t_kernel<float><<<dim3(cols / 64, rows / 64), 256, 0, s>>>(slab, splits, rows, cols, out, accumulate);
   return check_launch("splitk_reduce_t");
+}
+int splitk_reduce16_t(const bf16* slab, int splits, int rows, int cols, float* out, int accumulate, hipStream_t s) {
+  splitk_reduce_t_kernel<bf16><<<dim3(cols / 64, rows / 64), 256, 0, s>>>(slab, splits, rows, cols, out, accumulate);
+  return check_launch("splitk_reduce16_t");
+}
+int splitk_reduce16(const bf16* slab, int splits, size_t n, float* out, int accumulate, hipStream_t s) {
+  splitk_reduce16_kernel<<<2048, 256, 0, s>>>(slab, splits, n / 8, out, accumulate);
+  return check_launch("splitk_reduce16");
 }
 int splitk_reduce(const float* slab, int splits, size_t n, float* out, int accumulate, hipStream_t s) {
   splitk_reduce_kernel<<<2048, 256, 0, s>>>(slab, splits, n / 4, out, accumulate);

@@ -11,6 +11,7 @@ enum Epi : int {
                      //                               were folded into aux by the forward epilogue)
   EPI_ATOMIC = 5,    // atomicAdd(C_f32, alpha*acc)            (split-K wgrad into the grad arena)
   EPI_SLAB = 6,      // split-K partial tile -> fp32 slab[blockIdx.y] (gemm256 wgrad; summed by splitk_reduce)
+  EPI_SLAB16 = 7,    // the same partial tile rounded to a bf16 slab (GPT2MI_SCHED_BF16_SLABS; splitk_reduce16)
 };
 
 struct GemmParams {
@@ -239,6 +240,9 @@ int gemm256_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t 
 int gemm_pp_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t s, int splits, int map = 0,
                      bool persistent_ok = true);
 int splitk_reduce(const float* slab, int splits, size_t n, float* out, int accumulate, hipStream_t s);
+// the same sums over bf16 slabs (each element widened to fp32, then added in split order)
+int splitk_reduce16(const bf16* slab, int splits, size_t n, float* out, int accumulate, hipStream_t s);
 // out[c][r] (+)= sum_z slab[z][r][c]: slabs [splits][rows][cols] summed in split order and written transposed
 int splitk_reduce_t(const float* slab, int splits, int rows, int cols, float* out, int accumulate, hipStream_t s);
+int splitk_reduce16_t(const bf16* slab, int splits, int rows, int cols, float* out, int accumulate, hipStream_t s);
 }

@@ -810,6 +810,9 @@ write_image(mi, wr * 64);
       if constexpr (EPI == EPI_SLAB) {
         float* slab = reinterpret_cast<float*>(P.C) + (size_t)split * P.M * P.ldc;
         store4<float>(slab + (size_t)gm * P.ldc + gn, v);
+      } else if constexpr (EPI == EPI_SLAB16) {  // 8 B per lane: one 512-B bf16 row per wave-instruction
+        bf16* slab = reinterpret_cast<bf16*>(P.C) + (size_t)split * P.M * P.ldc;
+        store4<bf16>(slab + (size_t)gm * P.ldc + gn, v);
       } else {
         constexpr int DROPM = (EPI == EPI_RESID || EPI == EPI_GELU) ? VC : -1;
         const f32x4 o = epilogue_apply<EPI, bf16, DROPM>(P, gm, gn, v, kOpnd ? opnd[it] : f32x4{0.f, 0.f, 0.f, 0.f});
@@ -949,11 +952,16 @@ int gemm_pp_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t 
   // one, 698-721 vs 765 TF). map 8 = the same (tools/lib_ab.py impl 8)
   if (layout == 2) {
     if (map != 0 && map != 8) return -1;
-    return epilogue == EPI_SLAB ? launch<true, true, EPI_SLAB>(P, s, splits)
-                                : epilogue == EPI_F32 ? launch<true, true, EPI_F32>(P, s, 1) : -1;
+    return epilogue == EPI_SLAB     ? launch<true, true, EPI_SLAB>(P, s, splits)
+           : epilogue == EPI_SLAB16 ? launch<true, true, EPI_SLAB16>(P, s, splits)
+           : epilogue == EPI_F32    ? launch<true, true, EPI_F32>(P, s, 1)
+                                    : -1;
   }
   // layout 1 split-K slabs: the weight gradient with its X operand transposed (gpt2mi_gemm_wgrad_kt)
-  if (layout == 1 && epilogue == EPI_SLAB) return P.N % BN == 0 ? launch<false, true, EPI_SLAB>(P, s, splits) : -1;
+  if (layout == 1 && (epilogue == EPI_SLAB || epilogue == EPI_SLAB16)) {
+    if (P.N % BN != 0) return -1;
+    return epilogue == EPI_SLAB ? launch<false, true, EPI_SLAB>(P, s, splits) : launch<false, true, EPI_SLAB16>(P, s, splits);
+  }
   if (map > 0 && epilogue == EPI_BF16 && layout <= 1 && P.N % BN == 0) {  // half-tile maps (tools/gemm_probe.py)
     if (layout == 0) {
       if (map == 1) return launch<false, false, EPI_BF16, 1>(P, s, 1);

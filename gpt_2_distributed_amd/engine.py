@@ -340,6 +340,10 @@ class Engine:
         # whose collectives overlap every pass, sets NO_PERSISTENT), gemm_sched for the running pass
         self.base_sched = K.SCHED_AUTO
         self.gemm_sched = K.SCHED_AUTO
+        # bf16 weight gradients (autocast): split-K partial sums rounded to bf16 slabs (gpt2mi.h
+        # GPT2MI_SCHED_BF16_SLABS; the reference's autocast wgrad rounds its whole sum to bf16 once): half the slab
+        # traffic. False: fp32 slabs (fp32-exact sums of the bf16 products)
+        self.wgrad_bf16_slabs = True
         if not hasattr(K, "load") or self.device.type != "cuda":
             raise RuntimeError("the engine needs the model on a cuda (MI355X) device")
         K.load()
@@ -356,11 +360,14 @@ class Engine:
     def _gemm(self, *a, **kw):
         K.gemm(*a, sched=self.gemm_sched, **kw)
 
-    def _gemm_wgrad(self, *a, **kw):
-        K.gemm_wgrad(*a, sched=self.gemm_sched, **kw)
+    def _wgrad_sched(self):
+        return self.gemm_sched | (K.SCHED_BF16_SLABS if self.wgrad_bf16_slabs else 0)
+
+    def _gemm_wgrad(self, *a, **kw):  # (bf16 operands only: the fp32 mode's wgrads run gemm layout 2)
+        K.gemm_wgrad(*a, sched=self._wgrad_sched(), **kw)
 
     def _gemm_wgrad_kt(self, *a, **kw):
-        K.gemm_wgrad_kt(*a, sched=self.gemm_sched, **kw)
+        K.gemm_wgrad_kt(*a, sched=self._wgrad_sched(), **kw)
 
     # ---- parameter views ------------------------------------------------------------------------------
     def p(self, name):  # fp32 master view

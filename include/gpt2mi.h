@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GPT2MI_ABI_VERSION 9
+#define GPT2MI_ABI_VERSION 10
 
 const char* gpt2mi_last_error(void);
 int gpt2mi_abi_version(void); /* returns GPT2MI_ABI_VERSION of the built library */
@@ -84,11 +84,17 @@ int gpt2mi_gemm(int layout, int epilogue, int M, int N, int K, const uint16_t* A
  *    8 = weight gradients on the ping-pong kernel (= auto). */
 #define GPT2MI_SCHED_AUTO 0
 #define GPT2MI_SCHED_NO_PERSISTENT 0x100
+/* GPT2MI_SCHED_BF16_SLABS (flag, gpt2mi_gemm_wgrad / gpt2mi_gemm_wgrad_kt only; v10): each split-K partial sum is
+ * rounded once to bf16 in its slab, then the slabs are summed in fp32 in split order (still deterministic) — half the
+ * slab write and reduce traffic. The reference's autocast weight gradient rounds its whole sum to bf16 once
+ * (torch.mm in bf16, cast to the fp32 .grad: train_gpt2_distributed.py:412); this rounds each of `splits` partial
+ * sums, an error of the same order. Without the flag the slabs are fp32 (fp32-exact weight gradients). */
+#define GPT2MI_SCHED_BF16_SLABS 0x200
 
 /* Weight gradient (train_gpt2_distributed.py:412 autograd wgrad of every nn.Linear):
  * C[M][N] (+)= alpha*(alpha_dev?) * A^T B, A stored [K][M] (dY), B stored [K][N] (X), K = tokens.
- * 256x256 tiles; `splits` K ranges write fp32 partial slabs to `workspace` (>= splits*M*N floats),
- * summed into C in a fixed order (deterministic). M, N, K multiples of 64; ldc == N. sched: as gpt2mi_gemm
+ * 256x256 tiles; `splits` K ranges write fp32 (GPT2MI_SCHED_BF16_SLABS: bf16) partial slabs to `workspace`
+ * (>= splits*M*N floats), summed into C in a fixed order (deterministic). M, N, K multiples of 64; ldc == N. sched: as gpt2mi_gemm
  * (the low byte 2 selects the 2-stage kernel). When M (N) is not a multiple of 256 (GPT-2 1.5B: 1600, 4800) the
  * partial last tile reads A (B) up to 192 elements past the end of its last row: the caller's allocation must
  * extend that far (the values are not used). */

@@ -727,6 +727,46 @@ def test_wgrad_full_size_vs_fp64(m, n):
         assert torch.equal(C, C2)
 
 
+@pytest.mark.parametrize("m,n,tokens,splits", [(2304, 768, 8192, 4), (768, 3072, 8192, 8), (4800, 1600, 4096, 3),
+                                               (1600, 6400, 2048, 2), (50432, 768, 4096, 3), (512, 192, 1024, 1)])
+def test_gemm_wgrad_bf16_slabs_vs_fp64(m, n, tokens, splits):
+    """GPT2MI_SCHED_BF16_SLABS (the engine's autocast weight gradients): every split-K partial sum rounded once to bf16,
+    the slabs summed in fp32 in split order. Against float64: within the error of one bf16 rounding of the sum (the
+    reference's autocast wgrad rounds its whole sum to bf16 once, train_gpt2_distributed.py:412), write and accumulate,
+    partial last tiles (1.5B widths); deterministic (bitwise on a rerun); the transposed-X form gives the same bits;
+    one split (no slabs) gives exactly the fp32-slab path's bits."""
+    g = torch.Generator().manual_seed(m + n + tokens + 7 * splits)
+    A = _tail(bf(torch.randn(tokens, m, generator=g) * 0.1))
+    B = _tail(bf(torch.randn(tokens, n, generator=g)))
+    ws = torch.empty(max(4, splits * m * n), device=dev)
+    C0 = torch.randn(m, n, generator=g).to(dev)
+    f16 = L().SCHED_BF16_SLABS
+    rows = torch.cat([torch.arange(0, m, max(1, m // 24), device=dev), torch.arange(m - 8, m, device=dev)])
+    ref = 0.5 * (A[:, rows].double().t() @ B.double())
+    for acc in (False, True):
+        C1, C2, C3 = C0.clone(), C0.clone(), C0.clone()
+        L().gemm_wgrad(m, n, tokens, A, m, B, n, C1, n, accumulate=acc, alpha=0.5, workspace=ws, splits=splits,
+                       sched=f16)
+        L().gemm_wgrad(m, n, tokens, A, m, B, n, C2, n, accumulate=acc, alpha=0.5, workspace=ws, splits=splits,
+                       sched=f16)
+        L().gemm_wgrad(m, n, tokens, A, m, B, n, C3, n, accumulate=acc, alpha=0.5, workspace=ws, splits=splits)
+        torch.cuda.synchronize()
+        assert torch.equal(C1, C2)
+        want = ref + (C0[rows].double() if acc else 0)
+        err = rel_err((C1[rows].double() - (C0[rows].double() if acc else 0)).cpu(), ref.cpu())
+        assert err < (1e-5 if splits == 1 else 3e-3), (acc, err)
+        assert rel_err(C1[rows].double().cpu(), want.cpu()) < 3e-3
+        if splits == 1:
+            assert torch.equal(C1, C3)
+        if m % 256 == 0:
+            Bt = B.t().contiguous()
+            C4 = C0.clone()
+            L().gemm_wgrad_kt(m, n, tokens, A, m, Bt, tokens, C4, n, accumulate=acc, alpha=0.5, workspace=ws,
+                              splits=splits, sched=f16)
+            torch.cuda.synchronize()
+            assert torch.equal(C1, C4), (acc, (C1 - C4).abs().max().item())
+
+
 def test_lm_head_dgrad_full_size_vs_fp64():
     """dlnf = dlogits . wte at cfg 2's full size (65 536 x 768 over K = 50 432, the forward layout against the
     transposed wte shadow) against float64 on sampled rows."""
