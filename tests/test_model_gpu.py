@@ -365,12 +365,21 @@ def test_b64_step_equals_the_mean_of_b4_chunks():
     the 124M trajectory test pins to the reference: the B = 64 step's loss and every gradient equal the mean
     over its 16 B = 4 chunks. Exercises what only B = 64 reaches: the 6.6 GB logits / dlogits (> 4 GiB
     offsets), the lm_head wgrad split-K = 3 at M = 65536 and the 768-block attention map. The logits rows of
-    the first and last chunk are bit-identical to the B = 4 runs (same per-row GEMM)."""
+    the first and last chunk are bit-identical to the B = 4 runs (same per-row GEMM). Run with fp32 split-K slabs (the
+    sums exact to fp32 rounding, so 1e-3 bounds the chunking alone); the engine's default bf16 slabs (one bf16 rounding
+    of each partial sum, as the reference's autocast wgrad rounds its sum once) checked against them at 3e-3."""
     from gpt_2_distributed_amd.model import GPT2, GPT2Config
     m = GPT2(GPT2Config(resid_pdrop=0.0, attn_pdrop=0.0)).to(dev)
     g = torch.Generator().manual_seed(64)
     t = torch.randint(0, 50257, (64, 1025), generator=g).to(dev)
     x, y = t[:, :-1].contiguous(), t[:, 1:].contiguous()
+    m.engine().wgrad_bf16_slabs = True
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        _, loss16 = m(x, labels=y)
+    loss16.backward()
+    big16 = m.engine().grad.clone()
+    m.zero_grad(set_to_none=True)
+    m.engine().wgrad_bf16_slabs = False
     with torch.autocast("cuda", dtype=torch.bfloat16):
         logits, loss = m(x, labels=y)
     first, last = logits[:4].clone(), logits[60:].clone()
@@ -378,6 +387,13 @@ def test_b64_step_equals_the_mean_of_b4_chunks():
     loss.backward()
     big = m.engine().grad.clone()
     big_loss = loss.item()
+    assert loss16.item() == big_loss
+    for n, sl in m.layout.slots.items():
+        a = big16[sl.offset:sl.offset + sl.numel]
+        b = big[sl.offset:sl.offset + sl.numel]
+        e = float((a - b).double().norm() / (b.double().norm() + 1e-30))
+        assert e < 3e-3, ("bf16 slabs", n, e)
+    del big16
     m.zero_grad(set_to_none=True)
     chunk_losses = []
     for c in range(16):
