@@ -15,6 +15,8 @@ from gpt_2_distributed_amd import _lib as K  # noqa: E402
 from kbench import timeit, PEAK  # noqa: E402
 
 dev = "cuda"
+# SWEEP_SCHED=512: the engine's bf16 slabs (K.SCHED_BF16_SLABS)
+SCHED = int(os.environ.get("SWEEP_SCHED", "0"))
 
 
 def main(M=65536, C=768):
@@ -32,7 +34,7 @@ def main(M=65536, C=768):
         for _ in range(3):
             for s in cands:
                 ms = timeit(lambda: K.gemm_wgrad(m, n, M, A, m, B, n, Cm, n, accumulate=True, workspace=ws,  # noqa
-                                                 splits=s), reps=10)
+                                                 splits=s, sched=SCHED), reps=10)
                 best[s] = min(best.get(s, 1e9), ms)
         line = " ".join(f"{s}:{best[s]*1e3:.0f}" for s in cands)
         top = min(best, key=best.get)
