@@ -307,7 +307,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   // PERSIST: vector-memory stores each wave issues in an epilogue (one per output row and output array; the
   // column-sum atomic of waves 0-3 only makes the waits below retire more, never less)
   // (bf16 outputs: one 16-B store per lane and row pair, so half as many)
-  constexpr bool kWide = !AIL && (EPI == EPI_BF16 || EPI == EPI_GELU || EPI == EPI_GELU_BWD);
+  constexpr bool kWide = !AIL && (EPI == EPI_BF16 || EPI == EPI_GELU || EPI == EPI_GELU_BWD || EPI == EPI_SLAB16);
   constexpr int kStores = (EPI == EPI_GELU ? 64 : 32) / (kWide ? 2 : 1);
   bool after_epi = false;  // the current tile follows an epilogue (wave-uniform)
   f32x4 acc[2][2][4][2];
@@ -760,13 +760,18 @@ write_image(mi, wr * 64);
           f32x4 w0 = va[k], w1 = vb[k];
           w0 += bias;  // vector adds: packed without SLP
           w1 += bias1;
-          f32x4 r0, r1;
-          bf16x8 op = {};
-          if constexpr (EPI == EPI_GELU_BWD) op = op8[it];
-          epilogue8<EPI, EPI == EPI_GELU ? VC : 0>(P, gm, gnb, w0, w1, op, r0, r1);
-          if constexpr (kCsum && VC == 1) {  // vector adds: packed (v_pk_add_f32) without SLP, see the Makefile
-            csum += r0;
-            csum1 += r1;
+          if constexpr (EPI == EPI_SLAB16) {  // the split's bf16 slab: one 16-B store per lane and row
+            bf16* slab = reinterpret_cast<bf16*>(P.C) + (size_t)split * P.M * P.ldc;
+            store8_bf16(slab + (size_t)gm * P.ldc + gnb, w0, w1);
+          } else {
+            f32x4 r0, r1;
+            bf16x8 op = {};
+            if constexpr (EPI == EPI_GELU_BWD) op = op8[it];
+            epilogue8<EPI, EPI == EPI_GELU ? VC : 0>(P, gm, gnb, w0, w1, op, r0, r1);
+            if constexpr (kCsum && VC == 1) {  // vector adds: packed (v_pk_add_f32) without SLP, see the Makefile
+              csum += r0;
+              csum1 += r1;
+            }
           }
         }
         }
@@ -940,6 +945,11 @@ namespace gpt2mi {
 constexpr int g_persist_kmax = GPT2MI_PERSIST_KMAX;
 // Layouts 0 / 1; N % 256 == 0, every split's K range an even number (>= 2) of 64-deep tiles.
 // Returns -1 when this kernel does not apply (the caller falls back).
+// bf16-slab weight gradients: half-tile map 2 (A contiguous, B interleaved) so that the epilogue takes the wide path
+// (8 columns per lane, one 16-B store per row); map 3 (both interleaved, the fp32-slab kernel's) stores 8 B per lane
+#ifndef PP_WGRAD16_MAP
+#define PP_WGRAD16_MAP 2
+#endif
 int gemm_pp_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t s, int splits, int map,
                      bool persistent_ok) {
   // N (and M) multiples of 64; without split-K any K-tile count >= 2 (an odd count ends in a single K-tile); with
@@ -953,7 +963,7 @@ int gemm_pp_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t 
   if (layout == 2) {
     if (map != 0 && map != 8) return -1;
     return epilogue == EPI_SLAB     ? launch<true, true, EPI_SLAB>(P, s, splits)
-           : epilogue == EPI_SLAB16 ? launch<true, true, EPI_SLAB16>(P, s, splits)
+           : epilogue == EPI_SLAB16 ? launch<true, true, EPI_SLAB16, PP_WGRAD16_MAP>(P, s, splits)
            : epilogue == EPI_F32    ? launch<true, true, EPI_F32>(P, s, 1)
                                     : -1;
   }
