@@ -13,6 +13,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from gpt_2_distributed_amd import _lib as K  # noqa: E402
 
 dev = "cuda"
+# the weight gradients as the engine launches them under autocast: bf16 split-K slabs (KERNEL_ONE_FP32_SLABS=1: fp32)
+SLABS = 0 if os.environ.get("KERNEL_ONE_FP32_SLABS") == "1" else K.SCHED_BF16_SLABS
 M, C, Vp, V, B, T, H = 65536, 768, 50432, 50257, 64, 1024, 12
 
 
@@ -35,13 +37,13 @@ def make(name):
 
         def run():
             K.transpose_bf16(x, xt, M, C, C, M)
-            K.gemm_wgrad_kt(Vp, C, M, dl, Vp, xt, M, g, C, workspace=ws, splits=sp)
+            K.gemm_wgrad_kt(Vp, C, M, dl, Vp, xt, M, g, C, workspace=ws, splits=sp, sched=SLABS)
         return run
     if name == "lm_head_wgrad_old":
         dl, x, g = r(M, Vp), r(M, C), torch.zeros(Vp, C, device=dev)
         sp = K.wgrad_splits(Vp, C, M)
         ws = torch.empty(sp * Vp * C, device=dev)
-        return lambda: K.gemm_wgrad(Vp, C, M, dl, Vp, x, C, g, C, workspace=ws, splits=sp)
+        return lambda: K.gemm_wgrad(Vp, C, M, dl, Vp, x, C, g, C, workspace=ws, splits=sp, sched=SLABS)
     if name == "fc1_fwd":
         a, w = r(M, C), r(4 * C, C)
         bias = torch.zeros(4 * C, device=dev)
@@ -90,9 +92,9 @@ def make(name):
                 a, x, g = ops[(m, n)]
                 if m == Vp:
                     K.transpose_bf16(x, xt, M, C, C, M)
-                    K.gemm_wgrad_kt(m, n, M, a, m, xt, M, g, n, workspace=ws, splits=K.wgrad_splits(m, n, M))
+                    K.gemm_wgrad_kt(m, n, M, a, m, xt, M, g, n, workspace=ws, splits=K.wgrad_splits(m, n, M), sched=SLABS)
                 else:
-                    K.gemm_wgrad(m, n, M, a, m, x, n, g, n, workspace=ws, splits=K.wgrad_splits(m, n, M))
+                    K.gemm_wgrad(m, n, M, a, m, x, n, g, n, workspace=ws, splits=K.wgrad_splits(m, n, M), sched=SLABS)
         return run
     raise SystemExit(f"unknown kernel {name}")
 
