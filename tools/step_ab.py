@@ -4,6 +4,7 @@ dropout 0.1, fwd + loss + bwd + AdamW), rounds alternating between the settings,
     python tools/step_ab.py wgrad_bf16_slabs False True [--rounds 4 --steps 10]
 """
 import argparse
+import ast
 import os
 import sys
 import time
@@ -30,7 +31,7 @@ def main():
     g = torch.Generator().manual_seed(1234)
     t = torch.randint(0, cfg.vocab_size, (64, 1025), generator=g)
     x, y = t[:, :-1].contiguous().to(dev), t[:, 1:].contiguous().to(dev)
-    vals = [eval(v) for v in args.values]  # noqa: S307 (literals from the command line)
+    vals = [ast.literal_eval(v) for v in args.values]  # literals from the command line (True, 4, ...)
 
     def step():
         with torch.autocast("cuda", dtype=torch.bfloat16):
@@ -59,7 +60,7 @@ def main():
     for i, v in enumerate(vals):
         ms = sorted(res[i])
         print(f"{args.attr}={v!r:8}: ms/step {' '.join(f'{m:.2f}' for m in res[i])}  median {ms[len(ms) // 2]:.2f}  "
-              f"({64 * 1024 / ms[len(ms) // 2] * 1e3 / 1e6:.4f} M tok/s)  loss {float(loss):.4f}", flush=True)
+              f"({64 * 1024 / ms[len(ms) // 2] * 1e3 / 1e6:.4f} M tok/s)  loss {float(loss.detach()):.4f}", flush=True)
 
 
 if __name__ == "__main__":
