@@ -939,9 +939,11 @@ int launch_persistent(const GemmParams& P, hipStream_t s) {
 
 namespace gpt2mi {
 #ifndef GPT2MI_PERSIST_KMAX
-#define GPT2MI_PERSIST_KMAX 1024
+#define GPT2MI_PERSIST_KMAX 4096
 #endif
-// longest K that takes the persistent schedule by default (a tile's epilogue is a smaller share past it)
+// longest K that takes the persistent schedule by default: the step's K = 768 / 2304 / 3072 shapes (qkv / fc1 dgrad
+// and fc2 + residual 2-3 % faster than one tile per block since the persistent kernel reads the next K-tile's B
+// fragments in phase 4, tools/gemm_ab.py 0 7); the lm_head dgrad (K = 50 432) stays one tile per block
 constexpr int g_persist_kmax = GPT2MI_PERSIST_KMAX;
 // Layouts 0 / 1; N % 256 == 0, every split's K range an even number (>= 2) of 64-deep tiles.
 // Returns -1 when this kernel does not apply (the caller falls back).

@@ -517,16 +517,17 @@ def test_transpose_bf16_batched():
 
 
 @pytest.mark.parametrize("epi", ["plain", "bias", "gelu_drop", "resid_drop", "gelu_bwd_dbias"])
-@pytest.mark.parametrize("M,N", [(8192, 4096), (65536, 2304), (65536, 768)])
-def test_gemm_persistent_schedule_bitwise(epi, M, N):
+@pytest.mark.parametrize("M,N,K", [(8192, 4096, 768), (65536, 2304, 768), (65536, 768, 768), (65536, 768, 3072),
+                                   (16384, 768, 2304)])
+def test_gemm_persistent_schedule_bitwise(epi, M, N, K):
     """The persistent ping-pong schedule (short-K forward-layout GEMMs with >= 2 tiles per CU: one block per CU
     walks the tiles, the next tile's first K-tile lands during this tile's epilogue) computes every output
     element exactly as the one-tile-per-block kernel (sched 6 forces that one): bitwise equal,
     and within bf16 rounding of an fp32 reference on sampled rows. Covers every epilogue the step runs on it:
     plain / bias (qkv, proj dgrad), GELU + dropout (fc1), fp32 residual + dropout (proj forward) and the GELU
-    derivative product with its fused bias gradient (fc2 dgrad; column sums by atomics, so to fp32 rounding)."""
-    K = 768
-    g = torch.Generator().manual_seed(M + N)
+    derivative product with its fused bias gradient (fc2 dgrad; column sums by atomics, so to fp32 rounding). K = 2304 /
+    3072: the long-K shapes the persistent schedule also takes by default (qkv / fc1 dgrad, fc2 + residual)."""
+    g = torch.Generator().manual_seed(M + N + K)
     A = bf(torch.randn(M, K, generator=g)).to(dev)
     W = bf(torch.randn(N, K, generator=g) * 0.05).to(dev)
     bias = torch.randn(N, generator=g).to(dev) if epi not in ("plain", "gelu_bwd_dbias") else None

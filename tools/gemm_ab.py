@@ -28,6 +28,9 @@ def main():
         "qkv dgrad": (C, None, K.EPI_BF16, 3 * C),
         "fc1 dgrad": (C, None, K.EPI_BF16, 4 * C),
         "lm_head dgrad": (C, None, K.EPI_BF16, Vp),
+        "fc2 fwd +resid+drop": (C, True, K.EPI_RESID, 4 * C),
+        "proj fwd +resid+drop": (C, True, K.EPI_RESID, C),
+        "fc2 dgrad gelu-bwd": (4 * C, None, K.EPI_GELU_BWD, C),
     }
     if os.environ.get("GEMM_AB_SHAPES"):
         shapes = {k: v for k, v in shapes.items() if any(s in k for s in os.environ["GEMM_AB_SHAPES"].split(","))}
@@ -38,18 +41,22 @@ def main():
             xs[Kd] = rnd(M, Kd)
         W = rnd(N, Kd, sc=0.05)
         bias = torch.randn(N, device=dev) if has_bias else None
-        out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
-        aux = torch.empty(M, N, dtype=torch.bfloat16, device=dev) if epi == K.EPI_GELU else None
-        bufs[name] = (N, W, bias, out, aux, epi, Kd)
+        # EPI_RESID: fp32 out = resid + drop(acc + bias); EPI_GELU_BWD: bf16 out = acc * aux (the stored GELU derivative)
+        out = torch.empty(M, N, dtype=torch.float32 if epi == K.EPI_RESID else torch.bfloat16, device=dev)
+        aux = torch.empty(M, N, dtype=torch.bfloat16, device=dev) if epi in (K.EPI_GELU, K.EPI_GELU_BWD) else None
+        if epi == K.EPI_GELU_BWD:
+            aux.copy_(rnd(M, N))
+        resid = torch.randn(M, N, device=dev) if epi == K.EPI_RESID else None
+        bufs[name] = (N, W, bias, out, aux, resid, epi, Kd)
     res = {(n, i): [] for n in shapes for i in impls}
     ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
     for _ in range(5):
-        for name, (N, W, bias, out, aux, epi, Kd) in bufs.items():
+        for name, (N, W, bias, out, aux, resid, epi, Kd) in bufs.items():
             for impl in impls:
                 xa = xs[Kd]
-                fn = lambda: K.gemm(K.FWD, epi, M, N, Kd, xa, Kd, W, Kd, out, N, bias=bias, aux=aux,  # noqa: E731
-                                    ldaux=N if aux is not None else 0, p_drop=0.1 if aux is not None else 0.0, seed=5,
-                                    sched=impl)
+                drop = 0.1 if epi in (K.EPI_GELU, K.EPI_RESID) else 0.0
+                fn = lambda: K.gemm(K.FWD, epi, M, N, Kd, xa, Kd, W, Kd, out, N, bias=bias, resid=resid,  # noqa: E731
+                                    aux=aux, ldaux=N if aux is not None else 0, p_drop=drop, seed=5, sched=impl)
                 fn()
                 s, e = ev(), ev()
                 s.record()
