@@ -70,3 +70,12 @@ def test_gemm_schedule_is_a_per_call_argument():
     assert b"sched" in lib.gpt2mi_last_error()
     assert lib.gpt2mi_gemm_wgrad(256, 256, 64, None, 256, None, 256, None, 256, 0, 1.0, None, None, 0, 1, 0x1ff,
                                  None) == 22
+
+
+def test_schedule_flags_match_the_header():
+    """The GPT2MI_SCHED_* values the bindings pass (AUTO, NO_PERSISTENT, BF16_SLABS since v10) are the header's."""
+    from gpt_2_distributed_amd import _lib
+    src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    flags = {m.group(1): int(m.group(2), 0) for m in re.finditer(r"#define GPT2MI_SCHED_(\w+) (0x[0-9a-fA-F]+|\d+)", src)}
+    assert flags == {"AUTO": _lib.SCHED_AUTO, "NO_PERSISTENT": _lib.SCHED_NO_PERSISTENT,
+                     "BF16_SLABS": _lib.SCHED_BF16_SLABS}
