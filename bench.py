@@ -29,7 +29,16 @@ import torch
 import torch.distributed as dist
 
 PEAK_BF16_TFLOPS = 256 * 4 * 1024 * 2.4e9 / 1e12  # 2516.6 dense bf16 (MI355X_MICROARCH.md)
-METRIC = "train tokens/sec (whole node) + MFU, GPT-2 124M B=64 T=1024 at 1/2/4/8 MI355X"
+METRIC = "train tokens/sec (whole node) + MFU, GPT-2 124M B=64 T=1024 at 1/2/4/8 MI355X"  # BASELINE.json
+
+
+def metric_name(model, B, T, parallel, wrapped, GA):
+    """BASELINE.json's metric string for its headline configuration (124M, B=64, T=1024); the same metric named for
+    the configuration actually run otherwise (BASELINE cfgs 4 / 5: 350M / 1.5B under FSDP, accumulation)."""
+    if model == "124M" and B == 64 and T == 1024 and GA == 1 and not (wrapped and parallel == "fsdp"):
+        return METRIC
+    return (f"train tokens/sec (whole node) + MFU, GPT-2 {model} B={B} T={T}"
+            + (f" x{GA} accumulated" if GA > 1 else "") + (" FSDP" if wrapped and parallel == "fsdp" else ""))
 
 
 def flops_per_token(cfg, T):
@@ -166,25 +175,33 @@ def main():
                          "frac_of_peak": round(tf / PEAK_BF16_TFLOPS, 4)}
     dom = max(kernels, key=lambda k: kernels[k]["avg_ms"] * kernels[k]["launches"] / max(1, args.steps)) \
         if kernels else None
-    traffic = None
+    # roofline.traffic: the HBM bytes per launch of the dominant kernel from the PMC passes of THIS configuration
+    # (tools/pmc_traffic.sh -> profiles/traffic.json, collected at BASELINE cfg 2: 124M, B=64, T=1024); null for any
+    # other configuration (no PMC pass of its shapes), with the configuration the file's numbers belong to named
+    traffic, traffic_src = None, None
     tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "traffic.json")
+    cfg2 = args.model == "124M" and B == 64 and T == 1024
     if dom and os.path.exists(tpath):
         try:
-            traffic = json.load(open(tpath)).get(dom, {}).get("hbm_bytes_per_launch")
+            traffic = json.load(open(tpath)).get(dom, {}).get("hbm_bytes_per_launch") if cfg2 else None
         except Exception:
             traffic = None
+        traffic_src = ("profiles/traffic.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this configuration "
+                       "(124M, B=64, T=1024)" if traffic is not None else
+                       "null: profiles/traffic.json holds PMC passes of 124M, B=64, T=1024 only, not of this "
+                       "configuration's shapes")
     roofline = None
     if dom:
         k = kernels[dom]
         roofline = {"kernel": dom, "bound": "mfma", "achieved": k["tflops"], "peak": round(PEAK_BF16_TFLOPS, 1),
-                    "unit": "TFLOP/s", "frac": k["frac_of_peak"], "traffic": traffic,
+                    "unit": "TFLOP/s", "frac": k["frac_of_peak"], "traffic": traffic, "traffic_source": traffic_src,
                     "algorithmic_flop_per_launch": kflops[dom]}
 
     tokens = world * B * T * GA * args.steps
     tok_s = tokens / dt
     fpt = flops_per_token(cfg, T)
     out = {
-        "metric": METRIC,
+        "metric": metric_name(args.model, B, T, args.parallel, wrapped, GA),
         "value": round(tok_s, 1),
         "unit": "tokens/s",
         "n_gpus": world,

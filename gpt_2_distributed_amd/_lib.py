@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("GPT2MI_LIB") or os.path.join(_HERE, "libgpt2mi.so")
 
 # the ABI these bindings are written against (include/gpt2mi.h GPT2MI_ABI_VERSION): a stale or foreign
 # library is refused at load instead of being called with the wrong argument lists
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 _c_int, _c_float, _c_size, _c_u64, _p = ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_void_p
 

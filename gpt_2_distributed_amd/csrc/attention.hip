@@ -42,6 +42,10 @@ constexpr int BKV = 64;  // keys per K/V tile in fwd / dQ
 #ifndef ATTN_DKDV_WAVES
 #define ATTN_DKDV_WAVES 4
 #endif
+GPT2MI_PRODUCT_KNOB(ATTN_FWD_OCC, 3);
+GPT2MI_PRODUCT_KNOB(ATTN_FWD_LMAX, 1);
+GPT2MI_PRODUCT_KNOB(ATTN_DKDV_SB, 1);
+GPT2MI_PRODUCT_KNOB(ATTN_DKDV_WAVES, 4);
 constexpr int kDkdvWaves = ATTN_DKDV_WAVES;  // waves per dK/dV workgroup (32 keys each)
 constexpr int BKB = 32 * kDkdvWaves;        // keys per workgroup in dK/dV
 constexpr int BQT = 64;  // queries per Q/dO tile in dK/dV

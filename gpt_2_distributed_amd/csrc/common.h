@@ -16,6 +16,17 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 #define GPT2MI_EXPORT extern "C" __attribute__((visibility("default")))
 
+// A/B knobs (the -D macros tools/variant_lib.sh, tools/wgrad_ablation.sh and `make timing` build experiment libraries
+// with; some of them compile stores out or redirect them, i.e. give wrong outputs): the product library is built with
+// every knob at its product value, and a knob set to anything else without -DGPT2MI_AB_BUILD is a compile error, so
+// one stray -D cannot silently change what the step computes.
+#ifdef GPT2MI_AB_BUILD
+#define GPT2MI_PRODUCT_KNOB(name, value) static_assert(true, "")
+#else
+#define GPT2MI_PRODUCT_KNOB(name, value) \
+  static_assert((name) == (value), #name " is an A/B knob: build experiments with -DGPT2MI_AB_BUILD")
+#endif
+
 // ---- error reporting (C ABI: every entry returns 0 on success) ------------------------------
 namespace gpt2mi {
 void set_error(const char* fmt, ...);

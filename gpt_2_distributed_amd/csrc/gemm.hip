@@ -317,8 +317,10 @@ GPT2MI_EXPORT int gpt2mi_gemm_wgrad(int M, int N, int K, const uint16_t* A, int 
   const bool pp = (impl == 0 || impl == 8) && ktiles % 2 == 0;
   if (!pp && (M % 256 != 0 || N % 256 != 0 || impl == 1)) {
     // an odd token-tile count with a partial output tile: the 128x128 kernel (accumulates into / writes C, one pass)
+    // (impl 1 keeps forcing the 128x128 kernel there: gpt2mi_gemm would otherwise pick the ping-pong one)
     return gpt2mi_gemm(2, EPI_F32, M, N, K, A, lda, B, ldb, C, ldc, nullptr, nullptr, nullptr, 0, alpha, alpha_dev,
-                       accumulate, 1, 0.f, 0, nullptr, GPT2MI_SCHED_AUTO, stream);
+                       accumulate, 1, 0.f, 0, nullptr, (impl == 1 ? 1 : GPT2MI_SCHED_AUTO) | (sched & GPT2MI_SCHED_NO_PERSISTENT),
+                       stream);
   }
   int tiles_per = (ktiles + splits - 1) / splits;
   if (pp) tiles_per += tiles_per & 1;

@@ -62,9 +62,11 @@ __device__ __forceinline__ void dma_tile(const bf16* __restrict__ src, int ld, i
 #ifndef WG_BUFDMA
 #define WG_BUFDMA 1
 #endif
+GPT2MI_PRODUCT_KNOB(WG_BUFDMA, 1);
 #ifndef WG_ABL
 #define WG_ABL 0
 #endif
+GPT2MI_PRODUCT_KNOB(WG_ABL, 0);
 __device__ __forceinline__ uint32_t mc_lane_off(int ld, int wid, int par, int lane) {
   const int k = 8 * (wid & 1) + 2 * par + (lane >> 5);  // k-row mod 16 of instruction t = par (mod 2)
   return (uint32_t)(((lane >> 5) * ld + 8 * ((lane & 31) ^ mc_swz(k))) * (int)sizeof(bf16));

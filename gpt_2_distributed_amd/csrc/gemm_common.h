@@ -81,6 +81,7 @@ __device__ __forceinline__ void gelu4(f32x4 u, f32x4 m, f32x4& h, f32x4& d) {
 #ifndef GEMM_STORE_EXP
 #define GEMM_STORE_EXP 0
 #endif
+GPT2MI_PRODUCT_KNOB(GEMM_STORE_EXP, 0);
 __device__ __forceinline__ size_t out_idx(int gm, int ld, int gn) {
   if constexpr (GEMM_STORE_EXP == 2) return (size_t)(gm & 255) * ld + (gn & 255);
   return (size_t)gm * ld + gn;

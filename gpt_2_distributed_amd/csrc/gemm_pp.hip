@@ -46,6 +46,7 @@ constexpr int BM = 256, BN = 256, BK = 64;
 #ifndef PP_B0_EARLY
 #define PP_B0_EARLY 1
 #endif
+GPT2MI_PRODUCT_KNOB(PP_B0_EARLY, 1);
 constexpr int kThreads = 512;
 constexpr int kHalf = 128 * BK * 2;  // 16 KiB
 constexpr int kBuf = 4 * kHalf;      // A_0, A_1, B_0, B_1
@@ -75,8 +76,9 @@ __device__ __forceinline__ int half_map(int ir, int h) {
 //     is the same for every instruction, half and K-tile (one VGPR, dma_lane_off) and the instruction's position a
 //     wave-uniform 64-bit base in its descriptor (SALU), so the wgrad keeps no per-lane 64-bit pointers across the
 //     main loop (fits its 256 VGPRs with the phase-4 B reads, kEarly). A partial last tile (extent % 256 != 0, a
-//     multiple of 64) reads past the row's end — the next row's elements, and past the operand's last row up to 192
-//     elements (the caller's allocation covers them, gpt2mi.h); they only feed outputs the epilogue does not store.
+//     multiple of 64) reads past the row's end — the next row's elements, which only feed outputs the epilogue does
+//     not store; the descriptor's num_records ends at the operand's last element ((K - 1) * ld + extent), so
+//     lanes past the last row read zeros instead of whatever follows the operand in memory.
 // zero: the zero K-tile of an odd K-tile count (TRANS=0: every lane reads 16 zero bytes; TRANS=1: num_records 0).
 // 16 zero bytes: the source of every lane of a zero K-tile's flat DMAs
 __device__ const u32x4 g_zero16 = {0u, 0u, 0u, 0u};
@@ -101,7 +103,8 @@ __device__ __forceinline__ u32x4 buf_desc_n(const void* base, uint32_t bytes) {
 }
 template <bool TRANS, bool IS_A, bool IL>
 __device__ __forceinline__ void dma_half(const bf16* __restrict__ src, int ld, int base, int h, int k0, int rmax,
-                                         char* slot, int wid, int lane, uint32_t loff, bool zero = false) {
+                                         char* slot, int wid, int lane, uint32_t loff, int kdim,
+                                         bool zero = false) {
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     const int ins = wid * 2 + t;
@@ -116,8 +119,12 @@ __device__ __forceinline__ void dma_half(const bf16* __restrict__ src, int ld, i
       }
       lds_dma16(g, slot + ins * 1024);
     } else {
-      const bf16* g = src + (size_t)(k0 + 4 * ins) * ld + base + half_map<IL, IS_A>(0, h);
-      lds_dma16_buf(buf_desc_n(g, zero ? 0u : 0x7fffffffu), loff, 0, slot + ins * 1024);
+      // bytes from this instruction's base to the operand's last element ((kdim - 1) * ld + rmax + 1; uniform)
+      const int row = k0 + 4 * ins, col = base + half_map<IL, IS_A>(0, h);
+      const size_t rem = 2 * ((size_t)(kdim - 1 - row) * ld + (rmax + 1 - col));
+      const size_t off = (size_t)row * ld + col;
+      lds_dma16_buf(buf_desc_n(src + off, zero ? 0u : (uint32_t)min(rem, (size_t)0x7fffffffu)), loff, 0,
+                    slot + ins * 1024);
     }
   }
 }
@@ -202,6 +209,7 @@ constexpr int vm_cap(int n) { return n > 63 ? 63 : n; }
 #ifndef PP_LGKM_AFTER_BARRIER
 #define PP_LGKM_AFTER_BARRIER 1
 #endif
+GPT2MI_PRODUCT_KNOB(PP_LGKM_AFTER_BARRIER, 1);
 #if PP_LGKM_AFTER_BARRIER
 #define PP_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #else
@@ -245,6 +253,9 @@ __device__ __forceinline__ void lds_barrier() {
 // Timing instrumentation (tools/gemm_timing.py builds a separate library with -DGEMM_PP_TIMING): wave 0
 // of every block stamps s_memtime at kernel start (0), first operands landed (1), end of the main loop
 // (2) and end of the epilogue (3), plus its HW_ID / XCC_ID, into P.aux (BF16 epilogue only).
+#if defined(GEMM_PP_TIMING) && !defined(GPT2MI_AB_BUILD)
+#error "GEMM_PP_TIMING writes stamps into P.aux: an A/B build (make timing) only"
+#endif
 #ifdef GEMM_PP_TIMING
 #define PP_STAMP(I)                                                                                  \
   if (EPI == EPI_BF16 && P.aux && threadIdx.x == 0) {                                               \
@@ -263,6 +274,7 @@ __device__ __forceinline__ void lds_barrier() {
 #ifndef GPT2MI_PP_GM
 #define GPT2MI_PP_GM 4
 #endif
+GPT2MI_PRODUCT_KNOB(GPT2MI_PP_GM, 4);
 __device__ __forceinline__ void tile_of(int pid, int tiles_m, int tiles_n, int& m0, int& n0) {
   constexpr int GM = GPT2MI_PP_GM;
   const int group = pid / (GM * tiles_n);
@@ -347,24 +359,26 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
     if constexpr (PERSIST)
       dma_half_buf(rs_a, P.lda, mm0 + (h << 7), kofs(t), loff_a, buf + (h ? SA1 : SA0), wid);
     else
-      dma_half<A_T, true, AIL>(P.A, P.lda, mm0, h, kofs(t), P.M - 1, buf + (h ? SA1 : SA0), wid, lane, loff_a);
+      dma_half<A_T, true, AIL>(P.A, P.lda, mm0, h, kofs(t), P.M - 1, buf + (h ? SA1 : SA0), wid, lane, loff_a, P.K);
   };
   auto dma_b_at = [&](int nn0, int t, int h, char* buf) {
     if constexpr (PERSIST)
       dma_half_buf(rs_b, P.ldb, nn0 + (h << 7), kofs(t), loff_b, buf + (h ? SB1 : SB0), wid);
     else
-      dma_half<B_T, false, BIL>(P.B, P.ldb, nn0, h, kofs(t), P.N - 1, buf + (h ? SB1 : SB0), wid, lane, loff_b);
+      dma_half<B_T, false, BIL>(P.B, P.ldb, nn0, h, kofs(t), P.N - 1, buf + (h ? SB1 : SB0), wid, lane, loff_b, P.K);
   };
   auto dma_a = [&](int t, int h, char* buf) { dma_a_at(m0, t, h, buf); };
   auto dma_b = [&](int t, int h, char* buf) { dma_b_at(n0, t, h, buf); };
   // tile 0 of the prologue (zero source when odd; the persistent kernel never is)
   auto dma_a0z = [&](int t, int h, char* buf) {
     if constexpr (PERSIST) dma_a_at(m0, t, h, buf);
-    else dma_half<A_T, true, AIL>(P.A, P.lda, m0, h, kofs(t), P.M - 1, buf + (h ? SA1 : SA0), wid, lane, loff_a, odd);
+    else dma_half<A_T, true, AIL>(P.A, P.lda, m0, h, kofs(t), P.M - 1, buf + (h ? SA1 : SA0), wid, lane, loff_a, P.K,
+                                   odd);
   };
   auto dma_b0z = [&](int t, int h, char* buf) {
     if constexpr (PERSIST) dma_b_at(n0, t, h, buf);
-    else dma_half<B_T, false, BIL>(P.B, P.ldb, n0, h, kofs(t), P.N - 1, buf + (h ? SB1 : SB0), wid, lane, loff_b, odd);
+    else dma_half<B_T, false, BIL>(P.B, P.ldb, n0, h, kofs(t), P.N - 1, buf + (h ? SB1 : SB0), wid, lane, loff_b, P.K,
+                                    odd);
   };
   char* buf0 = smem;
   char* buf1 = smem + kBuf;
@@ -941,6 +955,7 @@ namespace gpt2mi {
 #ifndef GPT2MI_PERSIST_KMAX
 #define GPT2MI_PERSIST_KMAX 4096
 #endif
+GPT2MI_PRODUCT_KNOB(GPT2MI_PERSIST_KMAX, 4096);
 // longest K that takes the persistent schedule by default: the step's K = 768 / 2304 / 3072 shapes (qkv / fc1 dgrad
 // and fc2 + residual 2-3 % faster than one tile per block since the persistent kernel reads the next K-tile's B
 // fragments in phase 4, tools/gemm_ab.py 0 7); the lm_head dgrad (K = 50 432) stays one tile per block
@@ -952,6 +967,7 @@ constexpr int g_persist_kmax = GPT2MI_PERSIST_KMAX;
 #ifndef PP_WGRAD16_MAP
 #define PP_WGRAD16_MAP 2
 #endif
+GPT2MI_PRODUCT_KNOB(PP_WGRAD16_MAP, 2);
 int gemm_pp_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t s, int splits, int map,
                      bool persistent_ok) {
   // N (and M) multiples of 64; without split-K any K-tile count >= 2 (an odd count ends in a single K-tile); with

@@ -381,6 +381,7 @@ static int layernorm_bwd_t(const float* x, const float* w, const float* mean, co
 #ifndef LN_BWD_MAX_BLOCKS
 #define LN_BWD_MAX_BLOCKS 512
 #endif
+GPT2MI_PRODUCT_KNOB(LN_BWD_MAX_BLOCKS, 512);
   // the column-sum flush is one atomic per column per block: fewer blocks, fewer atomics (tools/ln_probe.py at cfg 2:
   // 2048 blocks 157-158 us, 1024 158, 512 153 — 8 waves per CU still stream at the HBM limit)
   const int g = grid_rows(M) > LN_BWD_MAX_BLOCKS ? LN_BWD_MAX_BLOCKS : grid_rows(M);

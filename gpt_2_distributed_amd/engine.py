@@ -70,10 +70,10 @@ def site_seeds(base_seed: int, step_seed: int, n_layer: int) -> dict:
     return s
 
 
-# Activation buffers carry this many elements of slack past their end: the weight-gradient GEMM of a width that is not
-# a multiple of 256 (GPT-2 1.5B: 1600, 4800) reads its partial last tile's columns up to 192 elements past the
-# operand's last row (gpt2mi.h gpt2mi_gemm_wgrad)
-ACT_TAIL = 256
+# Slack elements past the end of every activation buffer. None is needed since ABI v11: the weight-gradient GEMM of a
+# width that is not a multiple of 256 (GPT-2 1.5B: 1600, 4800) bounds its partial last tile's reads at the operand's
+# last element (gpt2mi.h gpt2mi_gemm_wgrad; v10 read up to 192 elements past it).
+ACT_TAIL = 0
 
 
 def act_empty(*shape, dtype, device):
@@ -151,7 +151,9 @@ class Scratch:
         wshapes = [(3 * C, C), (C, C), (4 * C, C), (C, 4 * C)] + ([(vpad, C)] if head else [])
         need = max((K_wgrad_splits(m, n, M) * m * n if K_wgrad_splits(m, n, M) > 1 else 0)
                    for m, n in wshapes) if C % 64 == 0 and act == BF16 else 0
-        if head and C % 64 == 0 and act == BF16:  # the lm_head's transposed-X wgrad always goes through its slabs
+        if head and C % 64 == 0 and act == BF16 and M % 128 == 0 and vpad % 256 == 0:
+            # the lm_head's transposed-X wgrad (taken under exactly these conditions, Engine._backward) always goes
+            # through its slabs
             need = max(need, K_wgrad_splits(vpad, C, M) * vpad * C)
         self.wgrad_ws = e(max(need, 4), dt=F32)
 
@@ -290,10 +292,12 @@ class GradHooks:
     def end_backward(self) -> None:
         """The backward's last kernel is enqueued: finish the collective before backward returns."""
 
-    def backward_sched(self, base: int) -> int:
-        """The GEMM schedule flags of this backward's launches (_lib.SCHED_*): a wrapper whose collectives run
-        concurrently with the backward keeps the persistent schedule off."""
-        return base
+    def inflight(self) -> bool:
+        """A collective of this wrapper may be running on its own stream concurrently with the kernels enqueued now.
+        The engine then launches its GEMMs without the persistent (one block per CU) schedule: a persistent block that
+        lands on a CU held by an RCCL kernel waits for it, and the whole grid ends on its latest block
+        (gpt2mi.h GPT2MI_SCHED_NO_PERSISTENT). Every other launch keeps the persistent schedule."""
+        return False
 
     def fwd_unit(self, unit: str) -> None:
         """FSDP: the parameters of ``unit`` ("embed", "h.<l>", "head") are about to be read."""
@@ -303,6 +307,12 @@ class Engine:
     """Owns the workspaces, the bf16 weight shadow and the grad arena of one GPT2 model."""
 
     WGRAD_SPLITS = 4
+    # Weight-gradient split-K partial sums in bf16 slabs (gpt2mi.h GPT2MI_SCHED_BF16_SLABS: half the slab traffic,
+    # ~0.5 ms per cfg-2 step) or fp32 slabs (fp32-exact sums of the bf16 products). Off by default since round 4: the
+    # reference's autocast wgrad rounds its whole sum once to bf16 (at most 2^-8 relative on every element), while one
+    # bf16 rounding per split leaves elements whose partial sums cancel with far larger relative errors
+    # (tests/test_kernels_gpu.py::test_wgrad_slab_precision_per_element_at_the_proj_shape, 28 splits).
+    WGRAD_BF16_SLABS = False
 
     def __init__(self, model):
         self.model = model
@@ -336,14 +346,13 @@ class Engine:
         self._params = list(model.parameters())
         self.params_by_name = dict(model.named_parameters())
         self.probes: Dict[str, list] = {}  # name -> [(start_event, end_event)] recorded when armed
-        # GEMM schedule flags passed with every launch (gpt2mi.h GPT2MI_SCHED_*): base_sched for this engine (FSDP,
-        # whose collectives overlap every pass, sets NO_PERSISTENT), gemm_sched for the running pass
+        # GEMM schedule flags passed with every launch (gpt2mi.h GPT2MI_SCHED_*): base_sched for this engine, gemm_sched
+        # for the running pass; a data-parallel wrapper adds NO_PERSISTENT while its collectives are in flight (_sched)
         self.base_sched = K.SCHED_AUTO
         self.gemm_sched = K.SCHED_AUTO
-        # bf16 weight gradients (autocast): split-K partial sums rounded to bf16 slabs (gpt2mi.h
-        # GPT2MI_SCHED_BF16_SLABS; the reference's autocast wgrad rounds its whole sum to bf16 once): half the slab
-        # traffic. False: fp32 slabs (fp32-exact sums of the bf16 products)
-        self.wgrad_bf16_slabs = True
+        # bf16 weight gradients (autocast): split-K partial sums in bf16 (True) or fp32 (False) slabs, see
+        # WGRAD_BF16_SLABS
+        self.wgrad_bf16_slabs = self.WGRAD_BF16_SLABS
         if not hasattr(K, "load") or self.device.type != "cuda":
             raise RuntimeError("the engine needs the model on a cuda (MI355X) device")
         K.load()
@@ -357,11 +366,19 @@ class Engine:
             return _NullCtx
         return _EventCtx(lst)
 
+    def _sched(self):
+        """The GEMM schedule flags of a launch enqueued now: the engine's own, plus NO_PERSISTENT while a data-parallel
+        wrapper's collective may run concurrently (GradHooks.inflight)."""
+        s = self.gemm_sched
+        if self.grad_sync is not None and self.grad_sync.inflight():
+            s |= K.SCHED_NO_PERSISTENT
+        return s
+
     def _gemm(self, *a, **kw):
-        K.gemm(*a, sched=self.gemm_sched, **kw)
+        K.gemm(*a, sched=self._sched(), **kw)
 
     def _wgrad_sched(self):
-        return self.gemm_sched | (K.SCHED_BF16_SLABS if self.wgrad_bf16_slabs else 0)
+        return self._sched() | (K.SCHED_BF16_SLABS if self.wgrad_bf16_slabs else 0)
 
     def _gemm_wgrad(self, *a, **kw):  # (bf16 operands only: the fp32 mode's wgrads run gemm layout 2)
         K.gemm_wgrad(*a, sched=self._wgrad_sched(), **kw)
@@ -503,8 +520,7 @@ class Engine:
         self._prepare_grads(act if full else None)
         self.bwd_act = act  # the precision of this backward's gradients (FSDP reduces in it)
         scale = self.grad_sync.begin_backward() if self.grad_sync is not None else 1.0
-        self.gemm_sched = self.grad_sync.backward_sched(self.base_sched) if self.grad_sync is not None \
-            else self.base_sched
+        self.gemm_sched = self.base_sched
         self.grad_dirty = True
         return scale
 
@@ -906,7 +922,7 @@ class Engine:
     def _to_act(xf, act):
         if act == F32:
             return xf
-        out = act_empty(*xf.shape, dtype=BF16, device=xf.device)  # (a weight-gradient operand: tail slack)
+        out = act_empty(*xf.shape, dtype=BF16, device=xf.device)
         K.cast_f32_bf16(xf, out, xf.numel())
         return out
 

@@ -194,11 +194,10 @@ class _DDPHooks(_DPHooks):
             self.reducer.reset()
         return super().begin_backward()
 
-    def backward_sched(self, base: int) -> int:
-        # the buckets' RCCL kernels run under the rest of the backward: no persistent GEMM grid there (a block
-        # waiting for a CU held by a collective would hold the whole grid back; gpt2mi.h GPT2MI_SCHED_NO_PERSISTENT)
-        from . import _lib as K
-        return base | K.SCHED_NO_PERSISTENT if self.sync and self.coll else base
+    def inflight(self) -> bool:
+        # from the first bucket on, RCCL runs under the rest of the backward (no persistent GEMM grid there); the
+        # lm_head backward and the last blocks' backward before the first full bucket keep the persistent schedule
+        return self.sync and self.coll and bool(self.reducer.works)
 
     def ready(self, name):
         if self.sync and self.coll:
@@ -292,6 +291,12 @@ class _FSDPHooks(_DPHooks):
     def fwd_unit(self, unit):
         self.fsdp._gather_for(unit)
 
+    def inflight(self) -> bool:
+        # a prefetched all-gather (forward: under every block but the last unit, the head) or a reduce-scatter (backward:
+        # from the last block's on) may run on RCCL's stream; the head's forward, xent and the lm_head backward run alone
+        f = self.fsdp
+        return f.coll and (bool(f._pending) or bool(f._rs_works))
+
 
 class FullyShardedDataParallel(nn.Module):
     """FULL_SHARD data parallelism over per-GPT2Block units (see the module docstring)."""
@@ -308,10 +313,6 @@ class FullyShardedDataParallel(nn.Module):
         self.coll = use_collectives(W)
         if self.coll:
             dist.broadcast(module.arena, src=0)
-            # prefetched all-gathers and reduce-scatters overlap the forward and the backward: no persistent
-            # GEMM grids on this engine (see _DDPHooks.backward_sched)
-            from . import _lib as K
-            eng.base_sched = eng.gemm_sched = K.SCHED_NO_PERSISTENT
         self.units = unit_ranges(module.layout, module.config.n_layer)
         self.plans, self.shard_total = plan_shards(self.units, W)
         self.plan = {p.name: p for p in self.plans}

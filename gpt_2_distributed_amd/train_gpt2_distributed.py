@@ -12,7 +12,9 @@ grad_accum micro-steps the fused AdamW step (which also yields the clip_grad_nor
 checkpoints every --save_every optimizer steps between barriers. Differences, all deliberate:
   * DDP syncs gradients only on the last micro-step (``no_sync`` elsewhere; same math);
   * logged tok/s is the whole-node SUM and MFU is reported (the reference averages per-GPU tok/s,
-    stats_tracker.py:25-34); host syncs happen only on log steps;
+    stats_tracker.py:25-34); host syncs happen only on log steps, which also carry the reference's epoch_time and
+    memory metrics (gpu_alloc_gb, gpu_reserved_gb, gpu_max_alloc_gb, gpu_utilization_pct, cpu_mb;
+    stats_tracker.py:265-364) with its reductions over ranks (no TensorBoard writer);
   * checkpoints are collective-correct under fsdp, and --resume restores model + optimizer + the
     dropout stream + the data position (the reference's load_checkpoint is a stub, :104-111).
 """
@@ -115,6 +117,27 @@ def load_checkpoint(model, opt, ckpt_dir: str):
     return st
 
 
+def memory_metrics(world: int) -> dict:
+    """The reference's memory metrics (stats_tracker.py:265-364: _collect_memory_metrics and its registry entries),
+    reduced over ranks as it reduces them: gpu_alloc_gb / gpu_reserved_gb / gpu_utilization_pct averaged, gpu_max_alloc_gb
+    the MAX, cpu_mb the SUM (host RSS of every process). GiB = 2^30 bytes, MB = 2^20 as there. Collective: every rank
+    calls it (on log steps only)."""
+    import psutil
+    gib = 1024 ** 3
+    alloc = torch.cuda.memory_allocated() / gib
+    total = torch.cuda.get_device_properties(torch.cuda.current_device()).total_memory / gib
+    v = torch.tensor([alloc, torch.cuda.memory_reserved() / gib, alloc / total * 100.0,
+                      psutil.Process().memory_info().rss / 2 ** 20], dtype=torch.float64, device="cuda")
+    mx = torch.tensor([torch.cuda.max_memory_allocated() / gib], dtype=torch.float64, device="cuda")
+    if dist.is_initialized() and world > 1:
+        dist.all_reduce(v)
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        v[:3] /= world
+    v, mx = v.tolist(), mx.item()
+    return {"gpu_alloc_gb": round(v[0], 3), "gpu_reserved_gb": round(v[1], 3), "gpu_max_alloc_gb": round(mx, 3),
+            "gpu_utilization_pct": round(v[2], 2), "cpu_mb": round(v[3], 1)}
+
+
 def main(argv=None):
     torch.manual_seed(SEED)
     os.environ.setdefault("PYTORCH_CUDA_ALLOC_CONF", "expandable_segments:True")
@@ -169,8 +192,12 @@ def main(argv=None):
         st = load_checkpoint(model, optim, args.resume)
         global_step = st["step"]
         start_epoch, skip = int(st.get("epoch", 0)), int(st.get("micro", 0))
-        if "worker_epoch" in st:
+        if st.get("worker_epoch") is not None:
             worker_epoch = int(st["worker_epoch"])
+        elif "worker_epoch" not in st and start_epoch > 0:
+            # a checkpoint from before worker_epoch was recorded: an uninterrupted run spawned its persistent workers
+            # in epoch 0 (the first epoch it iterated), so they replay epoch 0's order in every later epoch
+            worker_epoch = 0
     fpt = 6 * (config.n_layer * 12 * config.n_embd ** 2 + config.vocab_size * config.n_embd) + \
         12 * config.n_layer * args.seq_len * config.n_embd
     optim.zero_grad()
@@ -178,6 +205,7 @@ def main(argv=None):
     t_last, steps_since = time.perf_counter(), 0
     done, epoch, micro = False, start_epoch, 0
     for epoch in range(start_epoch, args.epochs):
+        t_epoch = time.perf_counter()  # the reference's epoch_time (stats_tracker.py:265-275): time in this epoch
         ds.set_epoch(epoch)  # as the reference; persistent workers keep the epoch they were spawned with
         if dl is not None:
             if worker_epoch is None:
@@ -214,11 +242,13 @@ def main(argv=None):
                 torch.cuda.synchronize()
                 now = time.perf_counter()
                 tps = tok_per_step * steps_since / (now - t_last)
+                mem = memory_metrics(world)
                 if is_primary():
                     print(json.dumps({"step": global_step, "loss": round(loss.item() * args.grad_accum_steps, 5),
                                       "grad_norm": round(float(optim.grad_norm.item()), 5), "lr": args.lr,
                                       "tok_per_s_node": round(tps, 1),
-                                      "mfu": round(tps * fpt / (world * PEAK_BF16), 4)}), flush=True)
+                                      "mfu": round(tps * fpt / (world * PEAK_BF16), 4),
+                                      "epoch_time": round(now - t_epoch, 2), **mem}), flush=True)
                 t_last, steps_since = now, 0
             if global_step % args.save_every == 0:
                 save_checkpoint(model, optim, global_step, args.save_dir,

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GPT2MI_ABI_VERSION 10
+#define GPT2MI_ABI_VERSION 11
 
 const char* gpt2mi_last_error(void);
 int gpt2mi_abi_version(void); /* returns GPT2MI_ABI_VERSION of the built library */
@@ -96,8 +96,8 @@ int gpt2mi_gemm(int layout, int epilogue, int M, int N, int K, const uint16_t* A
  * 256x256 tiles; `splits` K ranges write fp32 (GPT2MI_SCHED_BF16_SLABS: bf16) partial slabs to `workspace`
  * (>= splits*M*N floats), summed into C in a fixed order (deterministic). M, N, K multiples of 64; ldc == N. sched: as gpt2mi_gemm
  * (the low byte 2 selects the 2-stage kernel). When M (N) is not a multiple of 256 (GPT-2 1.5B: 1600, 4800) the
- * partial last tile reads A (B) up to 192 elements past the end of its last row: the caller's allocation must
- * extend that far (the values are not used). */
+ * partial last tile's reads are bounded by the operand's last element ((K-1)*lda + M, (K-1)*ldb + N; buffer
+ * num_records): no slack past the operands is needed (v11; v10 read up to 192 elements past the last row). */
 int gpt2mi_gemm_wgrad(int M, int N, int K, const uint16_t* A, int lda, const uint16_t* B, int ldb, float* C, int ldc,
                       int accumulate, float alpha, const float* alpha_dev, float* workspace, size_t workspace_floats,
                       int splits, int sched, void* stream);

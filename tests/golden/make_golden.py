@@ -24,6 +24,9 @@ Outputs (all small data files, no reference source):
   ddp124_golden.json the same identity at cfg 3's widths (GPT-2 124M: C=768, H=12, V=50257, T=1024) on 2 layers,
                     2 ranks x B=2, grad_accum=1, 3 steps, lr 1e-3, Zipf tokens stored in the file: the DDP test with
                     the default 64 MiB buckets.
+  cfg4_golden.json  the same identity at BASELINE cfg 4's widths (GPT-2 350M: C=1024, H=16, V=50257, T=1024) on 2
+                    layers, 2 ranks x B=1, grad_accum=2, 3 steps, lr 1e-3, Zipf tokens stored in the file: the FSDP
+                    (FULL_SHARD) test of the 350M configuration (train_gpt2_distributed.py:146-161).
 """
 from __future__ import annotations
 
@@ -183,6 +186,12 @@ def ddp124_golden():
                  seq_len=1024, steps=3, grad_accum=1, world=2, per_rank=2, lr=1e-3, seed=37)
 
 
+def cfg4_golden():
+    _wide_golden("cfg4_golden.json", dict(n_layer=2, n_head=16, n_embd=1024, vocab_size=50257, n_positions=1024,
+                                          resid_pdrop=0.0, attn_pdrop=0.0),
+                 seq_len=1024, steps=3, grad_accum=2, world=2, per_rank=1, lr=1e-3, seed=41)
+
+
 def init_124m():
     cfg = ref_model.GPT2Config(n_layer=12, n_head=12, n_embd=768, n_positions=1024, vocab_size=50257)
     m = ref_model.GPT2(cfg)
@@ -260,7 +269,7 @@ if __name__ == "__main__":
     a = ap.parse_args()
     jobs = {"tiny": tiny_fwd_bwd, "tinytraj": tiny_traj, "init": init_124m, "loader": loader_grid,
             "traj": traj_124m, "accum": tiny_accum, "ddp": ddp_golden, "cfg5": cfg5_golden,
-            "ddp124": ddp124_golden}
+            "ddp124": ddp124_golden, "cfg4": cfg4_golden}
     for k, fn in jobs.items():
         if a.only and k not in a.only.split(","):
             continue

@@ -18,10 +18,12 @@ Variants (one torch.distributed.run launch runs them all):
   fsdp/ckpt     fsdp save_checkpoint -> fresh model + wrapper -> load_checkpoint -> the next step equals
                 the uninterrupted run's
 
-The same worker runs two production-width goldens (tests/golden/make_golden.py, the reference itself on the
+The same worker runs three production-width goldens (tests/golden/make_golden.py, the reference itself on the
 concatenated batch, Zipf tokens stored in the file):
   cfg5_golden.json    BASELINE cfg 5's widths (GPT-2 1.5B: C=1600, H=25, V=50257) on 2 layers, T=256, grad_accum=2,
                       through FullyShardedDataParallel (2 gloo ranks on the GPU, and 1 forced-RCCL rank);
+  cfg4_golden.json    BASELINE cfg 4's widths (GPT-2 350M: C=1024, H=16, V=50257) on 2 layers, T=1024, B=1 per rank,
+                      grad_accum=2, through FullyShardedDataParallel (2 gloo ranks, and 1 forced-RCCL rank);
   ddp124_golden.json  cfg 3's widths (GPT-2 124M: C=768, H=12, V=50257, T=1024) on 2 layers, B=2 per rank, through
                       DistributedDataParallel with its default 64 MiB buckets.
 """
@@ -199,13 +201,16 @@ def test_rccl_collectives_vs_reference(rccl_results, variant):
     _check_vs_golden(rccl_results[variant], variant)
 
 
-CFG5 = json.load(open(os.path.join(GOLDEN, "cfg5_golden.json")))
-DDP124 = json.load(open(os.path.join(GOLDEN, "ddp124_golden.json")))
-WIDE_RUNS = {  # (golden, ranks, backend, variants, extra env)
-    "cfg5_gloo2": (CFG5, 2, "gloo", ["fsdp/fused/fp32", "fsdp/fused/bf16", "fsdp/torch/fp32"], {}),
-    "cfg5_rccl1": (CFG5, 1, "nccl", ["fsdp/fused/fp32", "fsdp/fused/bf16"], {}),
-    "ddp124_gloo2": (DDP124, 2, "gloo", ["ddp/fused/fp32", "ddp/fused/bf16", "ddp/torch/fp32"], {"BUCKET_MB": "64"}),
-    "ddp124_rccl1": (DDP124, 1, "nccl", ["ddp/fused/bf16"], {"BUCKET_MB": "64"}),
+WIDE = {name: json.load(open(os.path.join(GOLDEN, name)))
+        for name in ("cfg5_golden.json", "cfg4_golden.json", "ddp124_golden.json")}
+WIDE_RUNS = {  # (golden file, ranks, backend, variants, extra env)
+    "cfg5_gloo2": ("cfg5_golden.json", 2, "gloo", ["fsdp/fused/fp32", "fsdp/fused/bf16", "fsdp/torch/fp32"], {}),
+    "cfg5_rccl1": ("cfg5_golden.json", 1, "nccl", ["fsdp/fused/fp32", "fsdp/fused/bf16"], {}),
+    "cfg4_gloo2": ("cfg4_golden.json", 2, "gloo", ["fsdp/fused/fp32", "fsdp/fused/bf16", "fsdp/torch/fp32"], {}),
+    "cfg4_rccl1": ("cfg4_golden.json", 1, "nccl", ["fsdp/fused/fp32", "fsdp/fused/bf16"], {}),
+    "ddp124_gloo2": ("ddp124_golden.json", 2, "gloo", ["ddp/fused/fp32", "ddp/fused/bf16", "ddp/torch/fp32"],
+                     {"BUCKET_MB": "64"}),
+    "ddp124_rccl1": ("ddp124_golden.json", 1, "nccl", ["ddp/fused/bf16"], {"BUCKET_MB": "64"}),
 }
 
 
@@ -220,18 +225,17 @@ def wide_results(tmp_path_factory):
             env["GPT2MI_SINGLE_DEVICE"] = "1"
         else:
             env["GPT2MI_FORCE_COLLECTIVES"] = "1"
-        name = "cfg5_golden.json" if gold is CFG5 else "ddp124_golden.json"
-        out[run] = _launch(tmp_path_factory.mktemp(run), nproc, variants, 29560 + i, golden=name, **env)
+        out[run] = _launch(tmp_path_factory.mktemp(run), nproc, variants, 29560 + i, golden=gold, **env)
     return out
 
 
 @pytest.mark.parametrize("run,variant", [(r, v) for r, spec in WIDE_RUNS.items() for v in spec[3]])
 def test_production_width_vs_reference(wide_results, run, variant):
-    """BASELINE cfg 5 (1.5B widths, FSDP, grad_accum 2) and cfg 3 (124M widths, DDP, 64 MiB buckets) through the
-    wrappers against the reference on the concatenated batch: loss, grad norm and final parameters, fp32 within
-    1e-4 and bf16 autocast within 2e-2."""
+    """BASELINE cfg 5 (1.5B widths, FSDP, grad_accum 2), cfg 4 (350M widths, FSDP FULL_SHARD, grad_accum 2) and cfg 3
+    (124M widths, DDP, 64 MiB buckets) through the wrappers against the reference on the concatenated batch: loss,
+    grad norm and final parameters, fp32 within 1e-4 and bf16 autocast within 2e-2."""
     gold, nproc = WIDE_RUNS[run][0], WIDE_RUNS[run][1]
-    _check_vs_golden(wide_results[run][variant], variant, GOLD=gold, world=nproc)
+    _check_vs_golden(wide_results[run][variant], variant, GOLD=WIDE[gold], world=nproc)
 
 
 @pytest.mark.parametrize("parallel", ["ddp", "fsdp"])

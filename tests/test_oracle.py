@@ -237,11 +237,12 @@ def test_ddp_golden_is_the_concatenated_batch_run():
     _check_params(params, ref["params"], 1e-4)
 
 
-@pytest.mark.parametrize("name", ["cfg5_golden.json", "ddp124_golden.json"])
+@pytest.mark.parametrize("name", ["cfg5_golden.json", "cfg4_golden.json", "ddp124_golden.json"])
 def test_production_width_goldens_match_the_oracle(name):
     """The production-width goldens (the reference on the concatenated batch at GPT-2 1.5B widths with grad_accum 2,
-    and at 124M widths with T=1024) are what the oracle's loop computes from the stored tokens: pins the oracle at
-    the widths of BASELINE cfgs 3 and 5 (H=25 heads, C=1600, the full vocabulary)."""
+    at 350M widths with T=1024 and grad_accum 2, and at 124M widths with T=1024) are what the oracle's loop computes
+    from the stored tokens: pins the oracle at the widths of BASELINE cfgs 3, 4 and 5 (H=25 / 16 heads, C=1600 / 1024,
+    the full vocabulary)."""
     ref = json.load(open(os.path.join(GOLDEN, name)))
     cfg = model_ref.Cfg(**ref["config"])
     S, GA = ref["steps"], ref["grad_accum"]

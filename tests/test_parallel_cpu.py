@@ -73,6 +73,43 @@ def test_bucketed_allreduce_gloo():
         assert was_reset        # finish() leaves the reducer ready for the next backward
 
 
+def _ddp_inflight(rank, world):
+    """DDP's GEMM-schedule signal (GradHooks.inflight): False in the backward until the first bucket's all-reduce is
+    issued (the lm_head backward and the last blocks keep the persistent GEMM schedule), True while buckets are in
+    flight, False again after finish(); never in a no_sync micro-step."""
+    from gpt_2_distributed_amd.parallel import BucketedReducer, _DDPHooks
+
+    class _Eng:
+        grad_dirty = False
+    n = 8000
+    flat = torch.ones(n) / world
+    order = [(f"r{i}", i * 1000, (i + 1) * 1000) for i in reversed(range(8))]
+    red = BucketedReducer(flat, order, bucket_mb=2500 * 4 / 2**20)
+    hooks = _DDPHooks(_Eng(), world, red)
+    seen = []
+    hooks.begin_backward()
+    seen.append(hooks.inflight())
+    hooks.ready("r7")              # 1000 elements ready: below one bucket, nothing issued
+    seen.append(hooks.inflight())
+    hooks.ready("r6")
+    hooks.ready("r5")              # 3000 >= 2500: the first bucket goes out
+    seen.append(hooks.inflight())
+    hooks.end_backward()
+    seen.append(hooks.inflight())
+    hooks.sync = False
+    hooks.ready("r7")
+    seen.append(hooks.inflight())
+    return seen, bool(torch.allclose(flat, torch.ones(n)))
+
+
+def test_ddp_inflight_signal_gloo():
+    out = _spawn(_ddp_inflight)
+    for r, v in out.items():
+        assert isinstance(v, tuple), v
+        assert v[0] == [False, False, True, False, False], v
+        assert v[1]
+
+
 def test_backward_ready_order_is_contiguous():
     """The engine's ready events (head, h.L-1 .. h.0, embed) tile the arena contiguously in reverse order."""
     from gpt_2_distributed_amd.model import GPT2, GPT2Config

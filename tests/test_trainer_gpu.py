@@ -139,7 +139,8 @@ def test_trainer_cli_resume_in_a_later_epoch(tmp_path):
 
 def test_trainer_cli_end_to_end(tmp_path):
     """python -m gpt_2_distributed_amd.train_gpt2_distributed with the reference's flags on synthetic
-    shards: runs, logs JSON steps with a finite loss, and writes the checkpoint layout."""
+    shards: runs, logs JSON steps with a finite loss and the reference's epoch_time / memory metrics
+    (stats_tracker.py:265-364), and writes the checkpoint layout."""
     data, ckpt = tmp_path / "data", tmp_path / "ckpt"
     cmd = [sys.executable, "-m", "gpt_2_distributed_amd.train_gpt2_distributed", "--data_dir", str(data),
            "--synthetic", "2", "--synthetic_tokens", "60000", "--seq_len", "128", "--batch", "4",
@@ -150,5 +151,8 @@ def test_trainer_cli_end_to_end(tmp_path):
     steps = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
     assert [s["step"] for s in steps] == [1, 2, 3]
     assert all(0.0 < s["loss"] < 20.0 and s["tok_per_s_node"] > 0 for s in steps)
+    for s in steps:
+        assert 0 < s["gpu_alloc_gb"] <= s["gpu_max_alloc_gb"] and s["gpu_alloc_gb"] <= s["gpu_reserved_gb"]
+        assert 0 < s["gpu_utilization_pct"] < 100 and s["cpu_mb"] > 0 and s["epoch_time"] > 0
     for st in ("step_0000002", "step_0000003"):
         assert (ckpt / st / "model.pt").exists() and (ckpt / st / "optim.pt").exists()

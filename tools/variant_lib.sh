@@ -13,7 +13,7 @@ for f in runtime.cpp norm_embed.hip xent_adamw.hip gemm.hip gemm256.hip gemm_pp.
 done
 EXTRA=""; [ "$SRC" = attention.hip ] && EXTRA="-fno-honor-nans -fno-slp-vectorize"
 [ "$SRC" = gemm_pp.hip ] && EXTRA="-fno-slp-vectorize"
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++20 -Wall -Wno-unused-function -I../../include $EXTRA "$@" \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++20 -Wall -Wno-unused-function -I../../include -DGPT2MI_AB_BUILD $EXTRA "$@" \
   -c "$SRC" -o "build/${SRC}_$NAME.o"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "../../tools/ab/lib_$NAME.so" $OBJS "build/${SRC}_$NAME.o"
 echo "tools/ab/lib_$NAME.so"

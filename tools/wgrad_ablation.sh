@@ -8,7 +8,7 @@ mkdir -p ../../tools/ab
 OBJS="build/runtime.cpp.o build/norm_embed.hip.o build/xent_adamw.hip.o build/gemm.hip.o build/gemm_pp.hip.o build/attention.hip.o build/fp32.hip.o build/transpose.hip.o build/aux_ops.hip.o"
 for n in "$@"; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++20 -Wall -Wno-unused-function -I../../include \
-    -DWG_ABL=$n -c gemm256.hip -o build/gemm256_abl$n.o
+    -DGPT2MI_AB_BUILD -DWG_ABL=$n -c gemm256.hip -o build/gemm256_abl$n.o
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../../tools/ab/lib_abl$n.so $OBJS build/gemm256_abl$n.o
 done
 ls -la ../../tools/ab
