@@ -20,8 +20,8 @@ Replaces the reference's ``DDP(model, device_ids=[device])`` / ``FSDP(model, ...
   single ``flat_param``, like FSDP's FlatParameter with use_orig_params=False), its grad and the AdamW
   moments live only on the owning rank. In the forward the engine asks for each unit just before it
   reads it; the wrapper all-gathers that unit in the compute precision (bf16 under autocast, like
-  MixedPrecision(param_dtype=bf16)) and prefetches the NEXT unit's all-gather on RCCL's stream while
-  the current unit computes. In the backward each unit's gradient range is reduce-scattered (bf16
+  MixedPrecision(param_dtype=bf16)) and has the following units' all-gathers already in flight on RCCL's
+  stream (by default every remaining unit's, issued at the first unit: ``prefetch_depth``). In the backward each unit's gradient range is reduce-scattered (bf16
   under autocast, like reduce_dtype=bf16) the moment the engine marks it final, overlapped with the
   remaining backward. MI355X-first difference: a gathered unit stays resident until the next optimizer
   step (288 GB HBM holds every unit of every BASELINE model), so the backward does not re-gather it and
@@ -197,7 +197,8 @@ class _DDPHooks(_DPHooks):
     def inflight(self) -> bool:
         # from the first bucket on, RCCL runs under the rest of the backward (no persistent GEMM grid there); the
         # lm_head backward and the last blocks' backward before the first full bucket keep the persistent schedule
-        return self.sync and self.coll and bool(self.reducer.works)
+        # (a host-side event query: a bucket that reads complete is certainly done before anything enqueued now runs)
+        return self.sync and self.coll and any(not w.is_completed() for w in self.reducer.works)
 
     def ready(self, name):
         if self.sync and self.coll:
@@ -292,16 +293,21 @@ class _FSDPHooks(_DPHooks):
         self.fsdp._gather_for(unit)
 
     def inflight(self) -> bool:
-        # a prefetched all-gather (forward: under every block but the last unit, the head) or a reduce-scatter (backward:
-        # from the last block's on) may run on RCCL's stream; the head's forward, xent and the lm_head backward run alone
+        # an all-gather or reduce-scatter this wrapper issued has not completed yet (a host-side event query: when it
+        # reads complete, the collective is certainly done before anything enqueued now runs; while the host runs ahead
+        # of the GPU it may read pending for one that will be done by then, which only costs the persistent schedule)
         f = self.fsdp
-        return f.coll and (bool(f._pending) or bool(f._rs_works))
+        if not f.coll:
+            return False
+        return any(w is not None and not w.is_completed() for w, _ in f._pending.values()) or \
+            any(w is not None and not w.is_completed() for _, w, _ in f._rs_works)
 
 
 class FullyShardedDataParallel(nn.Module):
     """FULL_SHARD data parallelism over per-GPT2Block units (see the module docstring)."""
 
-    def __init__(self, module, device_ids=None, bucket_mb: float = 64.0, prefetch: bool = True):
+    def __init__(self, module, device_ids=None, bucket_mb: float = 64.0, prefetch: bool = True,
+                 prefetch_depth: Optional[int] = None):
         super().__init__()
         self.module = module
         eng = module.engine()
@@ -309,6 +315,10 @@ class FullyShardedDataParallel(nn.Module):
         self.world = dist.get_world_size()
         self.rank = dist.get_rank()
         self.prefetch = prefetch
+        # units gathered ahead of the one being computed (None: every remaining unit at the first unit's forward, so the
+        # gathers finish under the first blocks and the rest of the forward runs with no collective in flight; a
+        # gathered unit stays resident until the next optimizer step either way, so depth costs no memory)
+        self.prefetch_depth = prefetch_depth
         W, r = self.world, self.rank
         self.coll = use_collectives(W)
         if self.coll:
@@ -413,10 +423,10 @@ class FullyShardedDataParallel(nn.Module):
         if self._valid.get(unit) != dtype:
             if unit not in self._pending or self._pending[unit][1] != dtype:
                 self._issue_gather(unit, dtype)
-        if self.prefetch:  # the next unit's all-gather rides under this unit's compute
+        if self.prefetch:  # the next units' all-gathers ride under this unit's compute
             i = self.order.index(unit)
-            if i + 1 < len(self.order):
-                nxt = self.order[i + 1]
+            last = len(self.order) if self.prefetch_depth is None else min(len(self.order), i + 1 + self.prefetch_depth)
+            for nxt in self.order[i + 1:last]:
                 if self._valid.get(nxt) != dtype and nxt not in self._pending:
                     self._issue_gather(nxt, dtype)
         if self._valid.get(unit) == dtype:

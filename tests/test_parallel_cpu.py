@@ -75,8 +75,8 @@ def test_bucketed_allreduce_gloo():
 
 def _ddp_inflight(rank, world):
     """DDP's GEMM-schedule signal (GradHooks.inflight): False in the backward until the first bucket's all-reduce is
-    issued (the lm_head backward and the last blocks keep the persistent GEMM schedule), True while buckets are in
-    flight, False again after finish(); never in a no_sync micro-step."""
+    issued (the lm_head backward and the last blocks keep the persistent GEMM schedule), then True while a bucket has
+    not completed, False after finish(); never in a no_sync micro-step."""
     from gpt_2_distributed_amd.parallel import BucketedReducer, _DDPHooks
 
     class _Eng:
@@ -93,7 +93,7 @@ def _ddp_inflight(rank, world):
     seen.append(hooks.inflight())
     hooks.ready("r6")
     hooks.ready("r5")              # 3000 >= 2500: the first bucket goes out
-    seen.append(hooks.inflight())
+    seen.append(hooks.inflight() == any(not w.is_completed() for w in red.works) and len(red.works) == 1)
     hooks.end_backward()
     seen.append(hooks.inflight())
     hooks.sync = False
@@ -106,7 +106,7 @@ def test_ddp_inflight_signal_gloo():
     out = _spawn(_ddp_inflight)
     for r, v in out.items():
         assert isinstance(v, tuple), v
-        assert v[0] == [False, False, True, False, False], v
+        assert v[0] == [False, False, True, False, False], v  # (3rd: inflight tracks the bucket's completion)
         assert v[1]
 
 
