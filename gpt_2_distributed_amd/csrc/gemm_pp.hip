@@ -77,8 +77,10 @@ __device__ __forceinline__ int half_map(int ir, int h) {
 //     wave-uniform 64-bit base in its descriptor (SALU), so the wgrad keeps no per-lane 64-bit pointers across the
 //     main loop (fits its 256 VGPRs with the phase-4 B reads, kEarly). A partial last tile (extent % 256 != 0, a
 //     multiple of 64) reads past the row's end — the next row's elements, which only feed outputs the epilogue does
-//     not store; the descriptor's num_records ends at the operand's last element ((K - 1) * ld + extent), so
-//     lanes past the last row read zeros instead of whatever follows the operand in memory.
+//     not store; with BND (the launch has such a partial tile) the descriptor's num_records ends at the operand's last
+//     element ((K - 1) * ld + extent), so lanes past the last row read zeros instead of whatever follows the operand in
+//     memory. Full tiles never read past their rows: BND = false skips the bound, whose per-DMA scalar arithmetic cost
+//     the weight gradients 10-15 % (qkv 199 -> 236 us, tools/lib_ab.py, round 4).
 // zero: the zero K-tile of an odd K-tile count (TRANS=0: every lane reads 16 zero bytes; TRANS=1: num_records 0).
 // 16 zero bytes: the source of every lane of a zero K-tile's flat DMAs
 __device__ const u32x4 g_zero16 = {0u, 0u, 0u, 0u};
@@ -101,7 +103,7 @@ __device__ __forceinline__ u32x4 buf_desc_n(const void* base, uint32_t bytes) {
                (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32) & 0xffffu),
                (uint32_t)__builtin_amdgcn_readfirstlane(bytes), 0x00020000u};
 }
-template <bool TRANS, bool IS_A, bool IL>
+template <bool TRANS, bool IS_A, bool IL, bool BND>
 __device__ __forceinline__ void dma_half(const bf16* __restrict__ src, int ld, int base, int h, int k0, int rmax,
                                          char* slot, int wid, int lane, uint32_t loff, int kdim,
                                          bool zero = false) {
@@ -121,10 +123,14 @@ __device__ __forceinline__ void dma_half(const bf16* __restrict__ src, int ld, i
     } else {
       // bytes from this instruction's base to the operand's last element ((kdim - 1) * ld + rmax + 1; uniform)
       const int row = k0 + 4 * ins, col = base + half_map<IL, IS_A>(0, h);
-      const size_t rem = 2 * ((size_t)(kdim - 1 - row) * ld + (rmax + 1 - col));
       const size_t off = (size_t)row * ld + col;
-      lds_dma16_buf(buf_desc_n(src + off, zero ? 0u : (uint32_t)min(rem, (size_t)0x7fffffffu)), loff, 0,
-                    slot + ins * 1024);
+      if constexpr (BND) {
+        const size_t rem = 2 * ((size_t)(kdim - 1 - row) * ld + (rmax + 1 - col));
+        lds_dma16_buf(buf_desc_n(src + off, zero ? 0u : (uint32_t)min(rem, (size_t)0x7fffffffu)), loff, 0,
+                      slot + ins * 1024);
+      } else {
+        lds_dma16_buf(buf_desc_n(src + off, zero ? 0u : 0x7fffffffu), loff, 0, slot + ins * 1024);
+      }
     }
   }
 }
@@ -215,15 +221,17 @@ GPT2MI_PRODUCT_KNOB(PP_LGKM_AFTER_BARRIER, 1);
 #else
 #define PP_LGKM0()
 #endif
+#define PP_PRIO_HI() __builtin_amdgcn_s_setprio(1);
+#define PP_PRIO_LO() __builtin_amdgcn_s_setprio(0);
 #define PP_SYNC_MFMA(ACC, NI, VM)                          \
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM) : "memory"); \
   __builtin_amdgcn_sched_barrier(0);                       \
   __builtin_amdgcn_s_barrier();                            \
   PP_LGKM0()                                               \
   __builtin_amdgcn_sched_barrier(0);                       \
-  __builtin_amdgcn_s_setprio(1);                           \
+  PP_PRIO_HI()                                             \
   mfma_quadrant<NI>(ACC, fr);                              \
-  __builtin_amdgcn_s_setprio(0);                           \
+  PP_PRIO_LO()                                             \
   __builtin_amdgcn_sched_barrier(0);                       \
   __builtin_amdgcn_s_barrier();                            \
   __builtin_amdgcn_sched_barrier(0);
@@ -236,9 +244,9 @@ GPT2MI_PRODUCT_KNOB(PP_LGKM_AFTER_BARRIER, 1);
   __builtin_amdgcn_s_barrier();                                                       \
   PP_LGKM0()                                                                          \
   __builtin_amdgcn_sched_barrier(0);                                                  \
-  __builtin_amdgcn_s_setprio(1);                                                      \
+  PP_PRIO_HI()                                                                        \
   mfma_quadrant<NI>(ACC, fr);                                                         \
-  __builtin_amdgcn_s_setprio(0);                                                      \
+  PP_PRIO_LO()                                                                        \
   __builtin_amdgcn_sched_barrier(0);                                                  \
   __builtin_amdgcn_s_barrier();                                                       \
   __builtin_amdgcn_sched_barrier(0);
@@ -289,7 +297,8 @@ __device__ __forceinline__ void tile_of(int pid, int tiles_m, int tiles_n, int& 
 // through buffer 1 (a 64-row fp32 image, four passes), so the operand latency of a tile start and the
 // block launch gap overlap the epilogue instead of following it (the K = 768 shapes spend ~8 us of ~25
 // per tile there). Layout-0 shapes without split-K only (host-selected).
-template <bool A_T, bool B_T, int EPI, int MAP, bool PERSIST = false>
+// BND: a transposed operand has a partial last tile (M or N not a multiple of 256): its DMA is bounded (dma_half)
+template <bool A_T, bool B_T, int EPI, int MAP, bool PERSIST = false, bool BND = false>
 __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   PP_STAMP(0)
   constexpr bool AIL = MAP & 1, BIL = MAP & 2;  // interleaved half-tile maps (A/B experiments)
@@ -359,25 +368,25 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
     if constexpr (PERSIST)
       dma_half_buf(rs_a, P.lda, mm0 + (h << 7), kofs(t), loff_a, buf + (h ? SA1 : SA0), wid);
     else
-      dma_half<A_T, true, AIL>(P.A, P.lda, mm0, h, kofs(t), P.M - 1, buf + (h ? SA1 : SA0), wid, lane, loff_a, P.K);
+      dma_half<A_T, true, AIL, BND>(P.A, P.lda, mm0, h, kofs(t), P.M - 1, buf + (h ? SA1 : SA0), wid, lane, loff_a, P.K);
   };
   auto dma_b_at = [&](int nn0, int t, int h, char* buf) {
     if constexpr (PERSIST)
       dma_half_buf(rs_b, P.ldb, nn0 + (h << 7), kofs(t), loff_b, buf + (h ? SB1 : SB0), wid);
     else
-      dma_half<B_T, false, BIL>(P.B, P.ldb, nn0, h, kofs(t), P.N - 1, buf + (h ? SB1 : SB0), wid, lane, loff_b, P.K);
+      dma_half<B_T, false, BIL, BND>(P.B, P.ldb, nn0, h, kofs(t), P.N - 1, buf + (h ? SB1 : SB0), wid, lane, loff_b, P.K);
   };
   auto dma_a = [&](int t, int h, char* buf) { dma_a_at(m0, t, h, buf); };
   auto dma_b = [&](int t, int h, char* buf) { dma_b_at(n0, t, h, buf); };
   // tile 0 of the prologue (zero source when odd; the persistent kernel never is)
   auto dma_a0z = [&](int t, int h, char* buf) {
     if constexpr (PERSIST) dma_a_at(m0, t, h, buf);
-    else dma_half<A_T, true, AIL>(P.A, P.lda, m0, h, kofs(t), P.M - 1, buf + (h ? SA1 : SA0), wid, lane, loff_a, P.K,
+    else dma_half<A_T, true, AIL, BND>(P.A, P.lda, m0, h, kofs(t), P.M - 1, buf + (h ? SA1 : SA0), wid, lane, loff_a, P.K,
                                    odd);
   };
   auto dma_b0z = [&](int t, int h, char* buf) {
     if constexpr (PERSIST) dma_b_at(n0, t, h, buf);
-    else dma_half<B_T, false, BIL>(P.B, P.ldb, n0, h, kofs(t), P.N - 1, buf + (h ? SB1 : SB0), wid, lane, loff_b, P.K,
+    else dma_half<B_T, false, BIL, BND>(P.B, P.ldb, n0, h, kofs(t), P.N - 1, buf + (h ? SB1 : SB0), wid, lane, loff_b, P.K,
                                     odd);
   };
   char* buf0 = smem;
@@ -777,6 +786,7 @@ write_image(mi, wr * 64);
           if constexpr (EPI == EPI_SLAB16) {  // the split's bf16 slab: one 16-B store per lane and row
             bf16* slab = reinterpret_cast<bf16*>(P.C) + (size_t)split * P.M * P.ldc;
             store8_bf16(slab + (size_t)gm * P.ldc + gnb, w0, w1);
+
           } else {
             f32x4 r0, r1;
             bf16x8 op = {};
@@ -924,6 +934,12 @@ write_image(mi, wr * 64);
 template <bool A_T, bool B_T, int EPI, int MAP = (A_T ? 1 : 0) | (B_T ? 2 : 0)>
 int launch(const GemmParams& P, hipStream_t s, int splits) {
   dim3 grid(((P.M + BM - 1) / BM) * ((P.N + BN - 1) / BN) * splits);
+  if constexpr (A_T || B_T) {  // a transposed operand with a partial last tile: the bounded DMA
+    if ((A_T && P.M % BM != 0) || (B_T && P.N % BN != 0)) {
+      gemm_pp_kernel<A_T, B_T, EPI, MAP, false, true><<<grid, kThreads, 0, s>>>(P);
+      return gpt2mi::check_launch("gemm_pp");
+    }
+  }
   gemm_pp_kernel<A_T, B_T, EPI, MAP><<<grid, kThreads, 0, s>>>(P);
   return gpt2mi::check_launch("gemm_pp");
 }
