@@ -30,6 +30,7 @@ struct GemmParams {
   uint64_t seed;
   uint32_t thr;
   float inv_keep;
+  int qslot;  // persistent schedule: this launch's work-queue slot (gemm_pp.hip g_pp_queue; set by the dispatcher)
 };
 
 // keep mask of the 4 dropout elements 2*pidx .. 2*pidx+3 as multipliers keep/(1-p) or 0 (x * m is the

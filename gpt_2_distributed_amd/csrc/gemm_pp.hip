@@ -33,6 +33,7 @@
 //    128 rows, 16-B chunk c of row r at c ^ (r & 15): conflict-free both ways), then every wave
 //    reads back whole rows and applies the fused epilogue with full-row coalesced stores (one
 //    store instruction = one 256-column output row).
+#include <atomic>
 #include <type_traits>
 
 #include "common.h"
@@ -278,6 +279,28 @@ __device__ __forceinline__ void lds_barrier() {
 #define PP_STAMP(I)
 #endif
 
+// Persistent schedule: the work queue. Items (output tiles) are dealt to the 8 XCD labels (blockIdx % 8) in contiguous
+// ranges, as xcd_remap does; the first two items of every block are static (blockIdx / 8 and that plus the blocks per
+// label), every later one is taken from its label's counter by one returning device-scope atomic (memory-side, so
+// coherent across the XCDs' L2s), issued two tiles ahead in an epilogue (its latency hides under the epilogue's stores).
+// A block that starts late — its CU held by an RCCL kernel of a data-parallel wrapper, or by any concurrent kernel — so
+// takes fewer tiles instead of making the grid end on its last one, and the persistent schedule needs no switch-off
+// while collectives run (ABI v11: GPT2MI_SCHED_NO_PERSISTENT is accepted and ignored by the persistent shapes).
+// One slot per launch, rotating over kQueueSlots (at most 4 kernels run at once per process: GPU_MAX_HW_QUEUES); the
+// last block out resets its slot to zero for the next launch that takes it.
+#ifndef PP_DYN
+#define PP_DYN 1
+#endif
+GPT2MI_PRODUCT_KNOB(PP_DYN, 1);
+constexpr int kQueueSlots = 256;
+__device__ unsigned g_pp_queue[kQueueSlots][16];  // [slot][XCD label 0..7, 8: blocks out]
+// item range of XCD label x over n items (xcd_remap's)
+__device__ __forceinline__ void xcd_range(int x, int n, int& base, int& cnt) {
+  const int q = n / 8, r = n % 8;
+  base = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+  cnt = q + (x < r ? 1 : 0);
+}
+
 // Output tile of item `pid` (GM M-tiles per group share their B tiles in L2).
 #ifndef GPT2MI_PP_GM
 #define GPT2MI_PP_GM 4
@@ -307,6 +330,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   // one-tile-per-block k-contiguous kernels keep the round-2 schedule (their per-lane flat DMA addresses would spill)
   constexpr bool kB0Early = PP_B0_EARLY && (PERSIST || (A_T && B_T));
   __shared__ __attribute__((aligned(1024))) char smem[kLds];
+  [[maybe_unused]] __shared__ int s_next;  // PERSIST, PP_DYN: the next tile's item, from the block's grab
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wid >> 2, wc = wid & 3;
@@ -319,6 +343,13 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   const int nsplit = PERSIST ? 1 : (P.K + P.k_per_split - 1) / P.k_per_split;
   int vid = blockIdx.x;  // PERSIST: virtual block id of this tile (blockIdx + i * gridDim, same XCD label)
   const int item = xcd_remap(vid, ntiles * nsplit);
+  // PERSIST, PP_DYN: the block's XCD label range and the item of its NEXT tile (the second one static)
+  [[maybe_unused]] int q_base = 0, q_cnt = 0, nxt_item = -1;
+  if constexpr (PERSIST && PP_DYN) {
+    xcd_range(blockIdx.x % 8, ntiles, q_base, q_cnt);
+    const int j1 = blockIdx.x / 8 + gridDim.x / 8;
+    nxt_item = j1 < q_cnt ? q_base + j1 : -1;
+  }
   const int split = item / ntiles;
   int m0, n0;
   tile_of(item - split * ntiles, tiles_m, tiles_n, m0, n0);
@@ -543,15 +574,29 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   if constexpr (PERSIST) {
     asm volatile("" ::"v"(bias[0]), "v"(bias[1]), "v"(bias[2]), "v"(bias[3]));
     if constexpr (kWide) asm volatile("" ::"v"(bias1[0]), "v"(bias1[1]), "v"(bias1[2]), "v"(bias1[3]));
-    vid += gridDim.x;
-    has_next = vid < ntiles;
+    int next_item;
+    if constexpr (PP_DYN) {
+      next_item = nxt_item;
+    } else {
+      vid += gridDim.x;
+      next_item = vid < ntiles ? xcd_remap(vid, ntiles) : -1;
+    }
+    has_next = next_item >= 0;
     if (has_next) {
-      tile_of(xcd_remap(vid, ntiles), tiles_m, tiles_n, next_m0, next_n0);
+      tile_of(next_item, tiles_m, tiles_n, next_m0, next_n0);
       dma_a_at(next_m0, 0, 0, buf0);
       dma_b_at(next_n0, 0, 0, buf0);
       dma_b_at(next_n0, 0, 1, buf0);
       dma_a_at(next_m0, 0, 1, buf0);
     }
+  }
+  // PP_DYN: the tile after next from the label's counter (one lane; read back at the end of this epilogue, by when the
+  // epilogue's stores have covered its latency)
+  [[maybe_unused]] unsigned grab = 0u;
+  if constexpr (PERSIST && PP_DYN) {
+    if (has_next && threadIdx.x == 0)
+      grab = __hip_atomic_fetch_add(&g_pp_queue[P.qslot][blockIdx.x % 8], 1u, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);
   }
 
   // ---- epilogue: acc[mi][ni][i][j][r] = C[m0 + mi*128 + wr*64 + 16i + (l&15)][n0 + ni*128 + wc*32 + 16j + 4(l>>4) + r]
@@ -902,11 +947,28 @@ write_image(mi, wr * 64);
   if constexpr (!PERSIST) {
     return;
   } else {
-    if (!has_next) return;
+    if (!has_next) {
+      if constexpr (PP_DYN) {
+        // the last block out (every block's grabs are done before it counts itself out) resets the slot
+        if (threadIdx.x == 0) {
+          unsigned* q = g_pp_queue[P.qslot];
+          if (__hip_atomic_fetch_add(q + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1)
+            for (int x = 0; x < 9; ++x) __hip_atomic_exchange(q + x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+      return;
+    }
+    if constexpr (PP_DYN) {  // the grabbed item for the tile after next, to every wave through LDS (barrier below)
+      if (threadIdx.x == 0) {
+        const int idx = (int)grab + 2 * (int)(gridDim.x / 8);
+        s_next = idx < q_cnt ? q_base + idx : -1;
+      }
+    }
     // the next tile's prologue continues: A_0 / B_0 of its K-tile 1 into buffer 1 once every wave is done
     // with the image there, then the same counted wait as the first prologue (epilogue stores issued in
     // between only make it wait longer, never too little: outstanding <= 8 leaves >= 4 DMAs retired)
     lds_barrier();
+    if constexpr (PP_DYN) nxt_item = __builtin_amdgcn_readfirstlane(s_next);
     m0 = next_m0;
     n0 = next_n0;
     zero_acc();
@@ -958,7 +1020,10 @@ int num_cus() {
 
 // persistent variant: one block per CU, grid a multiple of 8
 template <int EPI>
-int launch_persistent(const GemmParams& P, hipStream_t s) {
+int launch_persistent(const GemmParams& Pin, hipStream_t s) {
+  static std::atomic<unsigned> next_slot{0};
+  GemmParams P = Pin;
+  P.qslot = (int)(next_slot.fetch_add(1u, std::memory_order_relaxed) % kQueueSlots);
   const int ntiles = ((P.M + BM - 1) / BM) * (P.N / BN);  // N % 256 == 0 (gemm_pp_dispatch)
   dim3 grid(min(ntiles, num_cus()));
   gemm_pp_kernel<false, false, EPI, 0, true><<<grid, kThreads, 0, s>>>(P);

@@ -313,6 +313,10 @@ class Engine:
     # bf16 rounding per split leaves elements whose partial sums cancel with far larger relative errors
     # (tests/test_kernels_gpu.py::test_wgrad_slab_precision_per_element_at_the_proj_shape, 28 splits).
     WGRAD_BF16_SLABS = False
+    # GPT2MI_SCHED_NO_PERSISTENT while a data-parallel wrapper's collective may run (GradHooks.inflight). Off since ABI
+    # v11: the persistent GEMM takes its tiles from per-XCD work queues, so a block whose CU an RCCL kernel holds just
+    # takes fewer tiles (gemm_pp.hip g_pp_queue) and the persistent schedule stays on under collectives.
+    NO_PERSISTENT_UNDER_COLLECTIVES = False
 
     def __init__(self, model):
         self.model = model
@@ -370,7 +374,7 @@ class Engine:
         """The GEMM schedule flags of a launch enqueued now: the engine's own, plus NO_PERSISTENT while a data-parallel
         wrapper's collective may run concurrently (GradHooks.inflight)."""
         s = self.gemm_sched
-        if self.grad_sync is not None and self.grad_sync.inflight():
+        if self.NO_PERSISTENT_UNDER_COLLECTIVES and self.grad_sync is not None and self.grad_sync.inflight():
             s |= K.SCHED_NO_PERSISTENT
         return s
 
