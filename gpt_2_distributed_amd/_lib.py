@@ -135,6 +135,8 @@ FWD, DGRAD, WGRAD = 0, 1, 2
 # GEMM schedule per call (gpt2mi.h GPT2MI_SCHED_*): auto, or the flag that keeps the persistent schedule off while
 # RCCL kernels may share the CUs; the low byte picks a kernel for A/B experiments and kernel-equivalence tests
 SCHED_AUTO, SCHED_NO_PERSISTENT = 0, 0x100
+# other kernels (RCCL) may hold CUs: persistent GEMMs take tiles from work queues (gpt2mi.h GPT2MI_SCHED_SHARED_CUS)
+SCHED_SHARED_CUS = 0x400
 # gemm_wgrad / gemm_wgrad_kt: split-K partial sums rounded to bf16 slabs (gpt2mi.h GPT2MI_SCHED_BF16_SLABS)
 SCHED_BF16_SLABS = 0x200
 

@@ -223,7 +223,7 @@ GPT2MI_EXPORT int gpt2mi_gemm(int layout, int epilogue, int M, int N, int K, con
                  splits);
   GPT2MI_REQUIRE(splits == 1 || epilogue == EPI_ATOMIC, "gemm: split-K needs the atomic epilogue");
   GPT2MI_REQUIRE(layout >= 0 && layout <= 2, "gemm: bad layout %d", layout);
-  GPT2MI_REQUIRE((sched & ~(GPT2MI_SCHED_NO_PERSISTENT | 0xff)) == 0 && (sched & 0xff) <= 8, "gemm: bad sched %#x",
+  GPT2MI_REQUIRE((sched & ~(GPT2MI_SCHED_NO_PERSISTENT | GPT2MI_SCHED_SHARED_CUS | 0xff)) == 0 && (sched & 0xff) <= 8, "gemm: bad sched %#x",
                  sched);
   const int impl = sched & 0xff;
   GPT2MI_REQUIRE(ldc % 4 == 0 && (ldaux % 4 == 0 || aux == nullptr), "gemm: ldc/ldaux must be multiples of 4");
@@ -257,7 +257,8 @@ GPT2MI_EXPORT int gpt2mi_gemm(int layout, int epilogue, int M, int N, int K, con
   if (pp_ok && (impl == 0 || impl >= 3)) {
     // impl 6: the ping-pong kernel without its persistent schedule (A/B)
     const int map = impl == 6 ? -1 : impl == 7 ? 7 : (impl >= 3 && impl <= 5) ? impl - 2 : 0;
-    const int rc = gpt2mi::gemm_pp_dispatch(layout, epilogue, P, s, 1, map, !(sched & GPT2MI_SCHED_NO_PERSISTENT));
+    const int rc = gpt2mi::gemm_pp_dispatch(layout, epilogue, P, s, 1, map, !(sched & GPT2MI_SCHED_NO_PERSISTENT),
+                                            (sched & GPT2MI_SCHED_SHARED_CUS) != 0);
     if (rc >= 0) return rc;  // the ping-pong kernel fuses dbias
   }
   if (dbias) {  // other kernels: the GEMM, then the column sums of its output
@@ -299,7 +300,7 @@ GPT2MI_EXPORT int gpt2mi_gemm_wgrad(int M, int N, int K, const uint16_t* A, int 
                  "gemm_wgrad: M=%d N=%d K=%d must be multiples of 64", M, N, K);
   GPT2MI_REQUIRE(ldc == N, "gemm_wgrad: C must be dense (ldc == N)");
   GPT2MI_REQUIRE(splits >= 1 && splits <= K / 64, "gemm_wgrad: bad splits %d", splits);
-  GPT2MI_REQUIRE((sched & ~(GPT2MI_SCHED_NO_PERSISTENT | GPT2MI_SCHED_BF16_SLABS | 0xff)) == 0 && (sched & 0xff) <= 8,
+  GPT2MI_REQUIRE((sched & ~(GPT2MI_SCHED_NO_PERSISTENT | GPT2MI_SCHED_SHARED_CUS | GPT2MI_SCHED_BF16_SLABS | 0xff)) == 0 && (sched & 0xff) <= 8,
                  "gemm_wgrad: bad sched %#x", sched);
   const int impl = sched & 0xff;  // 2: the 2-stage 256x256 kernel (A/B); 0 / 8: the ping-pong kernel
   const bool slab16 = (sched & GPT2MI_SCHED_BF16_SLABS) != 0;
@@ -319,7 +320,8 @@ GPT2MI_EXPORT int gpt2mi_gemm_wgrad(int M, int N, int K, const uint16_t* A, int 
     // an odd token-tile count with a partial output tile: the 128x128 kernel (accumulates into / writes C, one pass)
     // (impl 1 keeps forcing the 128x128 kernel there: gpt2mi_gemm would otherwise pick the ping-pong one)
     return gpt2mi_gemm(2, EPI_F32, M, N, K, A, lda, B, ldb, C, ldc, nullptr, nullptr, nullptr, 0, alpha, alpha_dev,
-                       accumulate, 1, 0.f, 0, nullptr, (impl == 1 ? 1 : GPT2MI_SCHED_AUTO) | (sched & GPT2MI_SCHED_NO_PERSISTENT),
+                       accumulate, 1, 0.f, 0, nullptr, (impl == 1 ? 1 : GPT2MI_SCHED_AUTO) |
+                           (sched & (GPT2MI_SCHED_NO_PERSISTENT | GPT2MI_SCHED_SHARED_CUS)),
                        stream);
   }
   int tiles_per = (ktiles + splits - 1) / splits;
@@ -360,7 +362,7 @@ GPT2MI_EXPORT int gpt2mi_gemm_wgrad_kt(int M, int N, int K, const uint16_t* A, i
   GPT2MI_REQUIRE(M % 256 == 0, "gemm_wgrad_kt: M=%d must be a multiple of 256 (the transposed operand's full tiles)", M);
   GPT2MI_REQUIRE(ldc == N, "gemm_wgrad_kt: C must be dense (ldc == N)");
   GPT2MI_REQUIRE(splits >= 1 && splits <= K / 128, "gemm_wgrad_kt: bad splits %d", splits);
-  GPT2MI_REQUIRE((sched & ~(GPT2MI_SCHED_NO_PERSISTENT | GPT2MI_SCHED_BF16_SLABS | 0xff)) == 0,
+  GPT2MI_REQUIRE((sched & ~(GPT2MI_SCHED_NO_PERSISTENT | GPT2MI_SCHED_SHARED_CUS | GPT2MI_SCHED_BF16_SLABS | 0xff)) == 0,
                  "gemm_wgrad_kt: bad sched %#x", sched);
   const bool slab16 = (sched & GPT2MI_SCHED_BF16_SLABS) != 0;
   GPT2MI_REQUIRE(workspace != nullptr, "gemm_wgrad_kt: needs a workspace (splits*M*N floats)");

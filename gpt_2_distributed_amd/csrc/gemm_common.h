@@ -238,9 +238,11 @@ __device__ __forceinline__ void epilogue_store(const GemmParams& P, int gm, int 
 
 namespace gpt2mi {
 int gemm256_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t s, int splits);
-// persistent_ok: the caller allows the persistent (one block per CU) schedule (gpt2mi.h GPT2MI_SCHED_NO_PERSISTENT)
+// persistent_ok: the caller allows the persistent (one block per CU) schedule (gpt2mi.h GPT2MI_SCHED_NO_PERSISTENT);
+// shared_cus: other kernels (RCCL) may hold CUs: the persistent shapes take their tiles from work queues
+// (GPT2MI_SCHED_SHARED_CUS)
 int gemm_pp_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t s, int splits, int map = 0,
-                     bool persistent_ok = true);
+                     bool persistent_ok = true, bool shared_cus = false);
 int splitk_reduce(const float* slab, int splits, size_t n, float* out, int accumulate, hipStream_t s);
 // the same sums over bf16 slabs (each element widened to fp32, then added in split order)
 int splitk_reduce16(const bf16* slab, int splits, size_t n, float* out, int accumulate, hipStream_t s);

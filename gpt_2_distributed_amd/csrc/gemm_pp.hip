@@ -284,14 +284,11 @@ __device__ __forceinline__ void lds_barrier() {
 // label), every later one is taken from its label's counter by one returning device-scope atomic (memory-side, so
 // coherent across the XCDs' L2s), issued two tiles ahead in an epilogue (its latency hides under the epilogue's stores).
 // A block that starts late — its CU held by an RCCL kernel of a data-parallel wrapper, or by any concurrent kernel — so
-// takes fewer tiles instead of making the grid end on its last one, and the persistent schedule needs no switch-off
-// while collectives run (ABI v11: GPT2MI_SCHED_NO_PERSISTENT is accepted and ignored by the persistent shapes).
+// takes fewer tiles instead of making the grid end on its last one. Taken (DYN) when the caller says collectives may
+// share the CUs (gpt2mi.h GPT2MI_SCHED_SHARED_CUS): alone on the GPU the static walk is 1-3 % faster (the grab's wait
+// and LDS hand-off per tile; profiles/r4ab/gemm_dyn.log).
 // One slot per launch, rotating over kQueueSlots (at most 4 kernels run at once per process: GPU_MAX_HW_QUEUES); the
 // last block out resets its slot to zero for the next launch that takes it.
-#ifndef PP_DYN
-#define PP_DYN 1
-#endif
-GPT2MI_PRODUCT_KNOB(PP_DYN, 1);
 constexpr int kQueueSlots = 256;
 __device__ unsigned g_pp_queue[kQueueSlots][16];  // [slot][XCD label 0..7, 8: blocks out]
 // item range of XCD label x over n items (xcd_remap's)
@@ -321,7 +318,8 @@ __device__ __forceinline__ void tile_of(int pid, int tiles_m, int tiles_n, int& 
 // block launch gap overlap the epilogue instead of following it (the K = 768 shapes spend ~8 us of ~25
 // per tile there). Layout-0 shapes without split-K only (host-selected).
 // BND: a transposed operand has a partial last tile (M or N not a multiple of 256): its DMA is bounded (dma_half)
-template <bool A_T, bool B_T, int EPI, int MAP, bool PERSIST = false, bool BND = false>
+// DYN (PERSIST only): tiles from the work queue g_pp_queue (above) instead of the static walk
+template <bool A_T, bool B_T, int EPI, int MAP, bool PERSIST = false, bool BND = false, bool DYN = false>
 __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   PP_STAMP(0)
   constexpr bool AIL = MAP & 1, BIL = MAP & 2;  // interleaved half-tile maps (A/B experiments)
@@ -330,7 +328,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   // one-tile-per-block k-contiguous kernels keep the round-2 schedule (their per-lane flat DMA addresses would spill)
   constexpr bool kB0Early = PP_B0_EARLY && (PERSIST || (A_T && B_T));
   __shared__ __attribute__((aligned(1024))) char smem[kLds];
-  [[maybe_unused]] __shared__ int s_next;  // PERSIST, PP_DYN: the next tile's item, from the block's grab
+  [[maybe_unused]] __shared__ int s_next;  // PERSIST, DYN: the next tile's item, from the block's grab
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wid >> 2, wc = wid & 3;
@@ -343,9 +341,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   const int nsplit = PERSIST ? 1 : (P.K + P.k_per_split - 1) / P.k_per_split;
   int vid = blockIdx.x;  // PERSIST: virtual block id of this tile (blockIdx + i * gridDim, same XCD label)
   const int item = xcd_remap(vid, ntiles * nsplit);
-  // PERSIST, PP_DYN: the block's XCD label range and the item of its NEXT tile (the second one static)
+  // PERSIST, DYN: the block's XCD label range and the item of its NEXT tile (the second one static)
   [[maybe_unused]] int q_base = 0, q_cnt = 0, nxt_item = -1;
-  if constexpr (PERSIST && PP_DYN) {
+  if constexpr (PERSIST && DYN) {
     xcd_range(blockIdx.x % 8, ntiles, q_base, q_cnt);
     const int j1 = blockIdx.x / 8 + gridDim.x / 8;
     nxt_item = j1 < q_cnt ? q_base + j1 : -1;
@@ -575,7 +573,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
     asm volatile("" ::"v"(bias[0]), "v"(bias[1]), "v"(bias[2]), "v"(bias[3]));
     if constexpr (kWide) asm volatile("" ::"v"(bias1[0]), "v"(bias1[1]), "v"(bias1[2]), "v"(bias1[3]));
     int next_item;
-    if constexpr (PP_DYN) {
+    if constexpr (DYN) {
       next_item = nxt_item;
     } else {
       vid += gridDim.x;
@@ -590,10 +588,10 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
       dma_a_at(next_m0, 0, 1, buf0);
     }
   }
-  // PP_DYN: the tile after next from the label's counter (one lane; read back at the end of this epilogue, by when the
+  // DYN: the tile after next from the label's counter (one lane; read back at the end of this epilogue, by when the
   // epilogue's stores have covered its latency)
   [[maybe_unused]] unsigned grab = 0u;
-  if constexpr (PERSIST && PP_DYN) {
+  if constexpr (PERSIST && DYN) {
     if (has_next && threadIdx.x == 0)
       grab = __hip_atomic_fetch_add(&g_pp_queue[P.qslot][blockIdx.x % 8], 1u, __ATOMIC_RELAXED,
                                     __HIP_MEMORY_SCOPE_AGENT);
@@ -948,7 +946,7 @@ write_image(mi, wr * 64);
     return;
   } else {
     if (!has_next) {
-      if constexpr (PP_DYN) {
+      if constexpr (DYN) {
         // the last block out (every block's grabs are done before it counts itself out) resets the slot
         if (threadIdx.x == 0) {
           unsigned* q = g_pp_queue[P.qslot];
@@ -958,7 +956,7 @@ write_image(mi, wr * 64);
       }
       return;
     }
-    if constexpr (PP_DYN) {  // the grabbed item for the tile after next, to every wave through LDS (barrier below)
+    if constexpr (DYN) {  // the grabbed item for the tile after next, to every wave through LDS (barrier below)
       if (threadIdx.x == 0) {
         const int idx = (int)grab + 2 * (int)(gridDim.x / 8);
         s_next = idx < q_cnt ? q_base + idx : -1;
@@ -968,7 +966,7 @@ write_image(mi, wr * 64);
     // with the image there, then the same counted wait as the first prologue (epilogue stores issued in
     // between only make it wait longer, never too little: outstanding <= 8 leaves >= 4 DMAs retired)
     lds_barrier();
-    if constexpr (PP_DYN) nxt_item = __builtin_amdgcn_readfirstlane(s_next);
+    if constexpr (DYN) nxt_item = __builtin_amdgcn_readfirstlane(s_next);
     m0 = next_m0;
     n0 = next_n0;
     zero_acc();
@@ -1020,13 +1018,14 @@ int num_cus() {
 
 // persistent variant: one block per CU, grid a multiple of 8
 template <int EPI>
-int launch_persistent(const GemmParams& Pin, hipStream_t s) {
+int launch_persistent(const GemmParams& Pin, hipStream_t s, bool dyn) {
   static std::atomic<unsigned> next_slot{0};
   GemmParams P = Pin;
   P.qslot = (int)(next_slot.fetch_add(1u, std::memory_order_relaxed) % kQueueSlots);
   const int ntiles = ((P.M + BM - 1) / BM) * (P.N / BN);  // N % 256 == 0 (gemm_pp_dispatch)
   dim3 grid(min(ntiles, num_cus()));
-  gemm_pp_kernel<false, false, EPI, 0, true><<<grid, kThreads, 0, s>>>(P);
+  if (dyn) gemm_pp_kernel<false, false, EPI, 0, true, false, true><<<grid, kThreads, 0, s>>>(P);
+  else gemm_pp_kernel<false, false, EPI, 0, true><<<grid, kThreads, 0, s>>>(P);
   return gpt2mi::check_launch("gemm_pp_persistent");
 }
 
@@ -1050,7 +1049,7 @@ constexpr int g_persist_kmax = GPT2MI_PERSIST_KMAX;
 #endif
 GPT2MI_PRODUCT_KNOB(PP_WGRAD16_MAP, 2);
 int gemm_pp_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t s, int splits, int map,
-                     bool persistent_ok) {
+                     bool persistent_ok, bool shared_cus) {
   // N (and M) multiples of 64; without split-K any K-tile count >= 2 (an odd count ends in a single K-tile); with
   // split-K an even count per split
   if (P.N % 64 != 0 || P.M % 64 != 0 || P.K % BK != 0 || P.K < 2 * BK) return -1;
@@ -1096,10 +1095,10 @@ int gemm_pp_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t 
        epilogue == EPI_GELU_BWD) &&
       P.M % BM == 0 && (size_t)P.M * P.lda * 2 < (1ull << 31) && (size_t)P.N * P.ldb * 2 < (1ull << 31)) {
     switch (epilogue) {
-      case EPI_BF16: return launch_persistent<EPI_BF16>(P, s);
-      case EPI_GELU: return launch_persistent<EPI_GELU>(P, s);
-      case EPI_RESID: return launch_persistent<EPI_RESID>(P, s);
-      default: return launch_persistent<EPI_GELU_BWD>(P, s);
+      case EPI_BF16: return launch_persistent<EPI_BF16>(P, s, shared_cus);
+      case EPI_GELU: return launch_persistent<EPI_GELU>(P, s, shared_cus);
+      case EPI_RESID: return launch_persistent<EPI_RESID>(P, s, shared_cus);
+      default: return launch_persistent<EPI_GELU_BWD>(P, s, shared_cus);
     }
   }
   if (map < 0 || map == 7) map = 0;

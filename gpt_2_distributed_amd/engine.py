@@ -294,9 +294,9 @@ class GradHooks:
 
     def inflight(self) -> bool:
         """A collective of this wrapper may be running on its own stream concurrently with the kernels enqueued now.
-        The engine then launches its GEMMs without the persistent (one block per CU) schedule: a persistent block that
-        lands on a CU held by an RCCL kernel waits for it, and the whole grid ends on its latest block
-        (gpt2mi.h GPT2MI_SCHED_NO_PERSISTENT). Every other launch keeps the persistent schedule."""
+        The engine then launches its GEMMs with GPT2MI_SCHED_SHARED_CUS: the persistent (one block per CU) schedule
+        takes its tiles from per-XCD work queues, so a block that lands on a CU held by an RCCL kernel takes fewer
+        tiles instead of the whole grid ending on its latest block. Every other launch keeps the static walk."""
         return False
 
     def fwd_unit(self, unit: str) -> None:
@@ -313,10 +313,10 @@ class Engine:
     # bf16 rounding per split leaves elements whose partial sums cancel with far larger relative errors
     # (tests/test_kernels_gpu.py::test_wgrad_slab_precision_per_element_at_the_proj_shape, 28 splits).
     WGRAD_BF16_SLABS = False
-    # GPT2MI_SCHED_NO_PERSISTENT while a data-parallel wrapper's collective may run (GradHooks.inflight). Off since ABI
-    # v11: the persistent GEMM takes its tiles from per-XCD work queues, so a block whose CU an RCCL kernel holds just
-    # takes fewer tiles (gemm_pp.hip g_pp_queue) and the persistent schedule stays on under collectives.
-    NO_PERSISTENT_UNDER_COLLECTIVES = False
+    # Schedule flag added while a data-parallel wrapper's collective may run (GradHooks.inflight): since ABI v11
+    # GPT2MI_SCHED_SHARED_CUS (the persistent GEMM takes its tiles from per-XCD work queues, gemm_pp.hip g_pp_queue);
+    # v8-v10 passed GPT2MI_SCHED_NO_PERSISTENT (one tile per block) instead.
+    SCHED_UNDER_COLLECTIVES = K.SCHED_SHARED_CUS
 
     def __init__(self, model):
         self.model = model
@@ -351,7 +351,7 @@ class Engine:
         self.params_by_name = dict(model.named_parameters())
         self.probes: Dict[str, list] = {}  # name -> [(start_event, end_event)] recorded when armed
         # GEMM schedule flags passed with every launch (gpt2mi.h GPT2MI_SCHED_*): base_sched for this engine, gemm_sched
-        # for the running pass; a data-parallel wrapper adds NO_PERSISTENT while its collectives are in flight (_sched)
+        # for the running pass; a data-parallel wrapper adds SHARED_CUS while its collectives are in flight (_sched)
         self.base_sched = K.SCHED_AUTO
         self.gemm_sched = K.SCHED_AUTO
         # bf16 weight gradients (autocast): split-K partial sums in bf16 (True) or fp32 (False) slabs, see
@@ -371,11 +371,11 @@ class Engine:
         return _EventCtx(lst)
 
     def _sched(self):
-        """The GEMM schedule flags of a launch enqueued now: the engine's own, plus NO_PERSISTENT while a data-parallel
-        wrapper's collective may run concurrently (GradHooks.inflight)."""
+        """The GEMM schedule flags of a launch enqueued now: the engine's own, plus SCHED_UNDER_COLLECTIVES while a
+        data-parallel wrapper's collective may run concurrently (GradHooks.inflight)."""
         s = self.gemm_sched
-        if self.NO_PERSISTENT_UNDER_COLLECTIVES and self.grad_sync is not None and self.grad_sync.inflight():
-            s |= K.SCHED_NO_PERSISTENT
+        if self.grad_sync is not None and self.grad_sync.inflight():
+            s |= self.SCHED_UNDER_COLLECTIVES
         return s
 
     def _gemm(self, *a, **kw):

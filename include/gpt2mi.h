@@ -76,14 +76,16 @@ int gpt2mi_gemm(int layout, int epilogue, int M, int N, int K, const uint16_t* A
 /* GEMM schedule, chosen per call (v8; v7 had process-global switches):
  *  GPT2MI_SCHED_AUTO: the library picks the kernel (ping-pong 256x256; its persistent schedule for the short-K
  *    forward-layout shapes).
- *  GPT2MI_SCHED_NO_PERSISTENT (flag): never the persistent (one block per CU) schedule. The data-parallel wrappers
- *    pass it while their RCCL kernels may run concurrently: a persistent block that lands on a CU held by a
- *    collective waits for it, and the grid ends on its latest block.
+ *  GPT2MI_SCHED_NO_PERSISTENT (flag): never the persistent (one block per CU) schedule (one tile per block).
+ *  GPT2MI_SCHED_SHARED_CUS (flag, v11): other kernels (the data-parallel wrappers' RCCL collectives) may hold CUs while
+ *    this GEMM runs. The persistent schedule then takes its tiles from per-XCD work queues instead of a static walk:
+ *    a block whose CU a collective holds takes fewer tiles instead of making the grid end on its latest block.
  *  low byte (A/B experiments and the kernel-equivalence tests only): 1 = 128x128 kernel, 2 = 2-stage 256x256,
  *    3..5 = ping-pong with half-tile map 1..3, 6 = ping-pong one tile per block, 7 = persistent at any K,
  *    8 = weight gradients on the ping-pong kernel (= auto). */
 #define GPT2MI_SCHED_AUTO 0
 #define GPT2MI_SCHED_NO_PERSISTENT 0x100
+#define GPT2MI_SCHED_SHARED_CUS 0x400
 /* GPT2MI_SCHED_BF16_SLABS (flag, gpt2mi_gemm_wgrad / gpt2mi_gemm_wgrad_kt only; v10): each split-K partial sum is
  * rounded once to bf16 in its slab, then the slabs are summed in fp32 in split order (still deterministic) — half the
  * slab write and reduce traffic. The reference's autocast weight gradient rounds its whole sum to bf16 once

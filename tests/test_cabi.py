@@ -78,4 +78,4 @@ def test_schedule_flags_match_the_header():
     src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
     flags = {m.group(1): int(m.group(2), 0) for m in re.finditer(r"#define GPT2MI_SCHED_(\w+) (0x[0-9a-fA-F]+|\d+)", src)}
     assert flags == {"AUTO": _lib.SCHED_AUTO, "NO_PERSISTENT": _lib.SCHED_NO_PERSISTENT,
-                     "BF16_SLABS": _lib.SCHED_BF16_SLABS}
+                     "SHARED_CUS": _lib.SCHED_SHARED_CUS, "BF16_SLABS": _lib.SCHED_BF16_SLABS}

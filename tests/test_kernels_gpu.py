@@ -534,8 +534,8 @@ def test_gemm_persistent_schedule_bitwise(epi, M, N, K):
     resid = torch.randn(M, N, generator=g).to(dev) if epi == "resid_drop" else None
     dgelu = bf(torch.rand(M, N, generator=g) * 1.2 - 0.1).to(dev) if epi == "gelu_bwd_dbias" else None
     outs, dbs = [], []
-    # (0, NO_PERSISTENT): the data-parallel wrappers' schedule
-    for sched in (L().SCHED_AUTO, 6, L().SCHED_NO_PERSISTENT):
+    # SHARED_CUS: the work-queue persistent schedule the data-parallel wrappers take under collectives
+    for sched in (L().SCHED_AUTO, 6, L().SCHED_NO_PERSISTENT, L().SCHED_SHARED_CUS):
         C = torch.empty(M, N, dtype=torch.float32 if epi == "resid_drop" else torch.bfloat16, device=dev)
         if epi == "gelu_drop":
             aux = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
@@ -567,6 +567,34 @@ def test_gemm_persistent_schedule_bitwise(epi, M, N, K):
         full = outs[0][0].float().sum(0)  # the bias grad = column sums of the stored (bf16-rounded) output
         for db in dbs:
             assert torch.allclose(db, full, rtol=1e-4, atol=1e-3 * full.abs().max().item())
+
+
+def test_gemm_work_queue_reuse_across_streams():
+    """GPT2MI_SCHED_SHARED_CUS: the persistent GEMM's per-XCD work queues (gemm_pp.hip g_pp_queue, one slot per
+    launch over 256 rotating slots, reset by the last block out). 600 launches on two streams wrap the slots twice
+    with two grids running at once: every launch covers every tile exactly once (bitwise equal to the static walk),
+    so a slot left dirty or shared would show as a missing or doubled tile."""
+    M, N, K = 8192, 4096, 768
+    g = torch.Generator().manual_seed(5)
+    A = bf(torch.randn(M, K, generator=g)).to(dev)
+    W = bf(torch.randn(N, K, generator=g) * 0.05).to(dev)
+    ref = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    L().gemm(0, L().EPI_BF16, M, N, K, A, K, W, K, ref, N, sched=L().SCHED_AUTO)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = [torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=dev) for _ in range(4)]
+    torch.cuda.synchronize()
+    bad = 0
+    for i in range(600):
+        st = streams[i % 2]
+        C = outs[i % 4]
+        with torch.cuda.stream(st):
+            C.fill_(float("nan"))
+            L().gemm(0, L().EPI_BF16, M, N, K, A, K, W, K, C, N, sched=L().SCHED_SHARED_CUS)
+        if i % 50 == 49:
+            torch.cuda.synchronize()
+            bad += sum(int(not torch.equal(o, ref)) for o in outs)
+    torch.cuda.synchronize()
+    assert bad == 0
 
 
 @pytest.mark.parametrize("m,n,tokens,splits", [(2304, 768, 8192, 4), (768, 3072, 8192, 8), (50432, 768, 4096, 3)])
