@@ -346,6 +346,7 @@ class Engine:
         # that starts from zero_grad(set_to_none=True), which then zeroes only the accumulated slots
         self._grad_fresh = False
         self._acc_ranges = None     # cuda int64 [n, 2]: the arena ranges outside the GEMM-written weight slots
+        self._grad_dead = False     # discard_grads(): the arena restarts from zero at the next backward
         self.bwd_act = F32
         self._params = list(model.parameters())
         self.params_by_name = dict(model.named_parameters())
@@ -475,12 +476,19 @@ class Engine:
     def zero_grad(self):
         K.zero_(self.grad)
         self.grad_dirty = False
+        self._grad_dead = False
+
+    def discard_grads(self):
+        """The arena's gradients are consumed (FSDP reduced them into its shard): the next backward starts from zero,
+        zeroed lazily as after zero_grad(set_to_none=True) (a whole-model backward's weight-gradient GEMMs write their
+        slots and only the rest is zeroed)."""
+        self._grad_dead = True
+        self.grad_dirty = False
 
     def _lazy_zero_ok(self, act):
         # every weight-gradient GEMM of the full backward takes a path with a write-or-accumulate choice
-        # (gemm_wgrad / EPI_F32; not the EPI_ATOMIC fallback of widths that are not multiples of 64), and
-        # the arena is the engine's own (FSDP zeroes per unit)
-        return act == BF16 and self.param_provider is None and self.cfg.n_embd % 64 == 0
+        # (gemm_wgrad / EPI_F32; not the EPI_ATOMIC fallback of widths that are not multiples of 64)
+        return act == BF16 and self.cfg.n_embd % 64 == 0
 
     def _zero_accumulated(self):
         """Zero the arena outside the GEMM-written weight slots (wte with its pad rows, the four matrices of
@@ -504,7 +512,8 @@ class Engine:
         forms EVERY weight gradient (the whole-model loss backward): its GEMMs then write the weight slots
         and only the rest of the arena is zeroed."""
         self._grad_fresh = False
-        if all(p.grad is None for p in self.params_by_name.values()):
+        if self._grad_dead or all(p.grad is None for p in self.params_by_name.values()):
+            self._grad_dead = False
             if full_backward_act is not None and self._lazy_zero_ok(full_backward_act):
                 self._zero_accumulated()
                 self._grad_fresh = True

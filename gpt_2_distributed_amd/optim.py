@@ -34,13 +34,14 @@ class _FlatAdamW(torch.optim.Optimizer):
         self.step_count = 0
         self.grad_scale = 1.0
 
-    def _run(self, p, g, pb):
+    def _run(self, p, g, pb, lo=0, hi=None, grad_norm=None):
+        """One fused AdamW launch over p[lo:hi] (step_count advanced by the caller)."""
         grp = self.param_groups[0]
         b1, b2 = grp["betas"]
-        self.step_count += 1
-        K.adamw(p, g, self.exp_avg, self.exp_avg_sq, pb, p.numel(), float(grp["lr"]), float(grp["weight_decay"]),
-                float(b1), float(b2), float(grp["eps"]), self.step_count, float(self.grad_scale), self.partials,
-                self.grad_norm)
+        hi = p.numel() if hi is None else hi
+        K.adamw(p[lo:hi], g[lo:hi], self.exp_avg[lo:hi], self.exp_avg_sq[lo:hi], pb, hi - lo, float(grp["lr"]),
+                float(grp["weight_decay"]), float(b1), float(b2), float(grp["eps"]), self.step_count,
+                float(self.grad_scale), self.partials, self.grad_norm if grad_norm is None else grad_norm)
 
     def state_dict(self):
         return {"step": self.step_count, "exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq,
@@ -71,6 +72,7 @@ class FusedAdamW(_FlatAdamW):
         eng = self.engine
         if all(p.grad is None for p in eng.params_by_name.values()):
             return loss  # no gradients since zero_grad(set_to_none=True): torch's optimizers skip such params
+        self.step_count += 1
         self._run(self.model.arena, eng.grad, eng.shadow)
         eng.mark_shadow_fresh()
         return loss
@@ -88,9 +90,14 @@ class FusedAdamW(_FlatAdamW):
 
 
 class ShardedAdamW(_FlatAdamW):
+    """One launch per FSDP unit: each writes its unit's bf16 shard straight into that unit's all-gather buffer
+    (FullyShardedDataParallel.bf16_chunk), so the next forward gathers in place; the units' grad norms are combined
+    into the clip_grad_norm_ value."""
+
     def __init__(self, fsdp, lr=1e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1):
         super().__init__([fsdp.flat_param], fsdp.flat_param, lr, betas, eps, weight_decay)
         self.fsdp = fsdp
+        self.unit_norms = torch.zeros(len(fsdp.plans), dtype=torch.float32, device=fsdp.flat_param.device)
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -101,13 +108,17 @@ class ShardedAdamW(_FlatAdamW):
         f = self.fsdp
         if f.flat_param.grad is None:
             return loss  # no backward since zero_grad(set_to_none=True): skipped, as torch's optimizers do
-        self._run(f.flat_param.detach(), f.grad_shard, f.shard_bf16)
+        self.step_count += 1
+        p = f.flat_param.detach()
+        for i, q in enumerate(f.plans):
+            self._run(p, f.grad_shard, f.bf16_chunk(q.name), q.soff, q.soff + q.per, self.unit_norms[i:i + 1])
         f.mark_params_updated(bf16_fresh=True)
-        if f.coll:  # the clip_grad_norm_(inf) value of the full model: sum of squares over shards
-            n2 = self.grad_norm.square()
+        # the clip_grad_norm_(inf) value of the full model: sum of squares over units (and shards)
+        n2 = self.unit_norms.square().sum(0, keepdim=True)
+        if f.coll:
             dist.all_reduce(n2)
-            self.grad_norm.copy_(n2.sqrt())
+        torch.sqrt(n2, out=self.grad_norm)
         return loss
 
     def zero_grad(self, set_to_none: bool = True):
-        self.fsdp.zero_grad(set_to_none=False)
+        self.fsdp.zero_grad(set_to_none=set_to_none)

@@ -336,12 +336,12 @@ class FullyShardedDataParallel(nn.Module):
         # FSDP's FlatParameter (use_orig_params=False): the only parameter the wrapper exposes
         self.flat_param = nn.Parameter(master)
         self.grad_shard = torch.zeros_like(master)
-        self.shard_bf16 = torch.empty(self.shard_total, dtype=torch.bfloat16, device=dev)
         self._bufs: Dict[tuple, torch.Tensor] = {}
         self._valid: Dict[str, Optional[torch.dtype]] = {u: None for u in self.order}
         self._pending: Dict[str, tuple] = {}       # unit -> (work, dtype) of an in-flight all-gather
         self._rs_works: List[tuple] = []            # (unit, work, out) of in-flight reduce-scatters
-        self._bf16_fresh = False                     # shard_bf16 == bf16(flat_param) (set by our AdamW)
+        # every unit's bf16_chunk == bf16(its flat_param range) (set by our AdamW, which writes them)
+        self._bf16_fresh = False
         self._seen_version = None
         self.hooks = _FSDPHooks(self, W)
         # a torch optimizer on flat_param (fused AdamW does not bump its version): every gathered unit goes stale
@@ -380,9 +380,15 @@ class FullyShardedDataParallel(nn.Module):
             self._bufs[key] = t
         return t
 
+    def bf16_chunk(self, unit) -> torch.Tensor:
+        """This rank's bf16 shard of ``unit``: its chunk of the unit's all-gather buffer, so the bf16 gather runs in
+        place (RCCL copies nothing locally; at one rank the gathered unit IS the shard). The optimizer writes it."""
+        p = self.plan[unit]
+        return self._buf("ag", unit, torch.bfloat16, p.per * self.world)[self.rank * p.per:(self.rank + 1) * p.per]
+
     # ---- forward: per-unit all-gather with prefetch ---------------------------------------------------
     def mark_params_updated(self, bf16_fresh: bool):
-        """Called after an optimizer step on flat_param (our AdamW also wrote shard_bf16)."""
+        """Called after an optimizer step on flat_param (our AdamW also wrote every bf16_chunk)."""
         self._valid = {u: None for u in self.order}
         self._bf16_fresh = bf16_fresh
         self._seen_version = self.flat_param._version
@@ -400,16 +406,19 @@ class FullyShardedDataParallel(nn.Module):
     def _issue_gather(self, unit, dtype):
         from . import _lib as K
         p = self.plan[unit]
+        out = self._buf("ag", unit, dtype, p.per * self.world)
         if dtype == torch.bfloat16:
-            if not self._bf16_fresh:
-                K.cast_f32_bf16(self.flat_param.detach(), self.shard_bf16, self.shard_total)
+            if not self._bf16_fresh:  # a step we did not run (torch optimizer, load): re-round every shard
+                fp = self.flat_param.detach()
+                for q in self.plans:
+                    K.cast_f32_bf16(fp[q.soff:q.soff + q.per], self.bf16_chunk(q.name), q.per)
                 self._bf16_fresh = True
-            src = self.shard_bf16[p.soff:p.soff + p.per]
+            src = self.bf16_chunk(unit)  # in place: a view of out
         else:
             src = self.flat_param.detach()[p.soff:p.soff + p.per]
-        out = self._buf("ag", unit, dtype, p.per * self.world)
         if not self.coll:
-            out.copy_(src)
+            if src.data_ptr() != out.data_ptr():
+                out.copy_(src)
             work = None
         else:
             work = dist.all_gather_into_tensor(out, src, async_op=True)
@@ -451,9 +460,9 @@ class FullyShardedDataParallel(nn.Module):
         dtype = eng.bwd_act  # reduce_dtype = the compute precision (bf16 under autocast)
         inp = self._buf("rs_in", unit, dtype, p.per * self.world)
         K.fsdp_pack(eng.grad[p.lo:p.hi], inp, p.n, p.per * self.world)
-        out = self._buf("rs_out", unit, dtype, p.per)
+        # in place: this rank's chunk of the packed input receives the reduced shard (RCCL copies nothing locally)
+        out = inp[self.rank * p.per:(self.rank + 1) * p.per]
         if not self.coll:
-            out.copy_(inp)
             work = None
         else:
             work = dist.reduce_scatter_tensor(out, inp, op=dist.ReduceOp.SUM, async_op=True)
@@ -465,9 +474,9 @@ class FullyShardedDataParallel(nn.Module):
         for u in self.order:  # ranges the engine did not mark (e.g. a sub-module backward): reduce them too
             if u not in done:
                 self._reduce_scatter(u)
-        # the packed inputs hold this backward's gradients: the full arena restarts from zero
-        K.zero_(self.engine.grad)
-        self.engine.grad_dirty = False
+        # the packed inputs hold this backward's gradients: the full arena restarts from zero (lazily: the next
+        # backward's weight-gradient GEMMs write their slots and only the rest is zeroed, Engine.discard_grads)
+        self.engine.discard_grads()
         # accumulate only into a gradient the caller still holds: after a torch optimizer's
         # zero_grad(set_to_none=True) flat_param.grad is None and the shard's old values are stale
         acc = self.flat_param.grad is self.grad_shard
@@ -496,9 +505,12 @@ class FullyShardedDataParallel(nn.Module):
 
     def zero_grad(self, set_to_none: bool = True):
         from . import _lib as K
-        K.zero_(self.grad_shard)
-        self.flat_param.grad = None if set_to_none else self.grad_shard
-        self.engine.zero_grad()
+        if set_to_none:  # the next backward writes the shard instead of adding to it (_finish_reduce)
+            self.flat_param.grad = None
+        else:
+            K.zero_(self.grad_shard)
+            self.flat_param.grad = self.grad_shard
+        self.engine.discard_grads()
 
     def configure_optimizers(self, weight_decay=0.1, learning_rate=1e-4, betas=(0.9, 0.95), device_type=None,
                              eps=1e-8):

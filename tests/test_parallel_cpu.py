@@ -149,7 +149,9 @@ def test_shard_plan_any_world_size(world):
 def _shard_math(rank, world):
     """The FSDP collective pattern of one unit, in both reduce/param dtypes: a unit of n elements packed
     (zero-padded) to world*per, reduce-scattered (SUM of world-pre-divided grads) into this rank's per
-    chunk, and the chunks all-gathered back: the first n elements are the average, in unit order."""
+    chunk, and the chunks all-gathered back: the first n elements are the average, in unit order. Both
+    collectives run in place as the wrapper issues them (parallel.py _reduce_scatter: the shard is this rank's
+    chunk of the packed input; bf16_chunk: the gather source is this rank's chunk of the gather buffer)."""
     from gpt_2_distributed_amd.parallel import plan_shards
     ok = True
     n = 1000
@@ -157,10 +159,11 @@ def _shard_math(rank, world):
     for dt in (torch.float32, torch.bfloat16):
         g = torch.zeros(p.per * world, dtype=dt)
         g[:n] = (torch.arange(n, dtype=torch.float32) % 64 * (rank + 1) / world).to(dt)
-        shard = torch.empty(p.per, dtype=dt)
+        shard = g[rank * p.per:(rank + 1) * p.per]
         dist.reduce_scatter_tensor(shard, g, op=dist.ReduceOp.SUM)
-        full = torch.empty(p.per * world, dtype=dt)
-        dist.all_gather_into_tensor(full, shard)
+        full = torch.full((p.per * world,), float("nan"), dtype=dt)
+        full[rank * p.per:(rank + 1) * p.per] = shard
+        dist.all_gather_into_tensor(full, full[rank * p.per:(rank + 1) * p.per])
         exp = (torch.arange(n, dtype=torch.float32) % 64) * sum(range(1, world + 1)) / world
         tol = 1e-6 if dt == torch.float32 else 2e-2
         ok &= bool(torch.allclose(full[:n].float(), exp, rtol=tol, atol=tol)) and bool((full[n:] == 0).all())
