@@ -440,6 +440,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   PP_STAMP(1)
   if (wr == 1) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind group 0
   __builtin_amdgcn_sched_barrier(0);
+  // DYN: the queue counter's old value from this block's last grab (thread 0; written by an asm atomic, valid once a
+  // wait has retired it: read only at the end of the next main loop, after its vmcnt(0) waits)
+  [[maybe_unused]] unsigned grab = 0u;
   for (;;) {  // PERSIST: one iteration per output tile (non-persistent: exactly one)
 
   Frags fr;
@@ -519,9 +522,25 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   }
   ktile(nkv - 2, I0{}, Tr{}, F{});
   ktile(nkv - 2, I1{}, F{}, F{});
+  if constexpr (PERSIST && DYN) {
+    // the item of the tile after this one, from the grab of the last epilogue: the last K-tile's waits were vmcnt(0),
+    // so the atomic has returned (the empty asm keeps the read of `grab` below them)
+    if (after_epi) {
+      asm volatile("" : "+v"(grab));
+      if (threadIdx.x == 0) {
+        const int idx = (int)grab + 2 * (int)(gridDim.x / 8);
+        s_next = idx < q_cnt ? q_base + idx : -1;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+    }
+  }
   if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the groups (same barrier count)
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
+  if constexpr (PERSIST && DYN) {
+    asm volatile("" ::: "memory");
+    if (after_epi) nxt_item = __builtin_amdgcn_readfirstlane(s_next);
+  }
   PP_STAMP(2)
 
   // the thread index through an opaque copy: lane constants derived from it are formed here, per tile, instead of
@@ -588,13 +607,14 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
       dma_a_at(next_m0, 0, 1, buf0);
     }
   }
-  // DYN: the tile after next from the label's counter (one lane; read back at the end of this epilogue, by when the
-  // epilogue's stores have covered its latency)
-  [[maybe_unused]] unsigned grab = 0u;
+  // DYN: the tile after next from the label's counter (one lane; read back at the end of the next main loop). An asm
+  // atomic (relaxed, agent scope: sc0 returns the old value), so that no compiler-inserted vmcnt(0) drains this wave's
+  // DMAs and stores for its return (hipcc placed one right behind the builtin atomic: 1-3 % of the kernel)
   if constexpr (PERSIST && DYN) {
-    if (has_next && threadIdx.x == 0)
-      grab = __hip_atomic_fetch_add(&g_pp_queue[P.qslot][blockIdx.x % 8], 1u, __ATOMIC_RELAXED,
-                                    __HIP_MEMORY_SCOPE_AGENT);
+    if (has_next && threadIdx.x == 0) {
+      unsigned* qa = &g_pp_queue[P.qslot][blockIdx.x % 8];
+      asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(grab) : "v"(qa), "v"(1u) : "memory");
+    }
   }
 
   // ---- epilogue: acc[mi][ni][i][j][r] = C[m0 + mi*128 + wr*64 + 16i + (l&15)][n0 + ni*128 + wc*32 + 16j + 4(l>>4) + r]
@@ -956,17 +976,10 @@ write_image(mi, wr * 64);
       }
       return;
     }
-    if constexpr (DYN) {  // the grabbed item for the tile after next, to every wave through LDS (barrier below)
-      if (threadIdx.x == 0) {
-        const int idx = (int)grab + 2 * (int)(gridDim.x / 8);
-        s_next = idx < q_cnt ? q_base + idx : -1;
-      }
-    }
     // the next tile's prologue continues: A_0 / B_0 of its K-tile 1 into buffer 1 once every wave is done
     // with the image there, then the same counted wait as the first prologue (epilogue stores issued in
     // between only make it wait longer, never too little: outstanding <= 8 leaves >= 4 DMAs retired)
     lds_barrier();
-    if constexpr (DYN) nxt_item = __builtin_amdgcn_readfirstlane(s_next);
     m0 = next_m0;
     n0 = next_n0;
     zero_acc();
