@@ -46,6 +46,12 @@ GPT2MI_PRODUCT_KNOB(ATTN_FWD_OCC, 3);
 GPT2MI_PRODUCT_KNOB(ATTN_FWD_LMAX, 1);
 GPT2MI_PRODUCT_KNOB(ATTN_DKDV_SB, 1);
 GPT2MI_PRODUCT_KNOB(ATTN_DKDV_WAVES, 4);
+// A/B probe only (WRONG masks): the keep masks from bit-field extracts / shifts of a per-tile word instead of the counter
+// hash, pricing kernels that read precomputed mask bits
+#ifndef ATTN_BWD_MASK_PROBE
+#define ATTN_BWD_MASK_PROBE 0
+#endif
+GPT2MI_PRODUCT_KNOB(ATTN_BWD_MASK_PROBE, 0);
 constexpr int kDkdvWaves = ATTN_DKDV_WAVES;  // waves per dK/dV workgroup (32 keys each)
 constexpr int BKB = 32 * kDkdvWaves;        // keys per workgroup in dK/dV
 constexpr int BQT = 64;  // queries per Q/dO tile in dK/dV
@@ -333,8 +339,12 @@ __global__ __launch_bounds__(kThreads, ATTN_FWD_OCC) void attn_fwd_kernel(const 
 #pragma unroll
           for (int d = 0; d < 4; ++d) {  // dword d: keys (fi, r), (fi, r + 1) with fi = 2kk + (d >> 1), r = 2(d & 1)
             const uint32_t c = 16 * (2 * kk + (d >> 1)) + 2 * (d & 1);
+#if ATTN_BWD_MASK_PROBE
+            const uint32_t ka = pre << (c & 15), kb = pre << ((c + 1) & 15);
+#else
             const uint32_t ka = drop_keep_mask2(tk2, drop_fin(pre + c * kDropC1, seed_kx(seed)));
             const uint32_t kb = drop_keep_mask2(tk2, drop_fin(pre + (c + 1) * kDropC1, seed_kx(seed)));
+#endif
             // the bytes of each bf16 = the sign (keep bit) of key r's / key r+1's decision for query group 0 / 1
             w0[d] &= __builtin_amdgcn_perm(kb, ka, 0x0A0A0808u);
             w1[d] &= __builtin_amdgcn_perm(kb, ka, 0x0B0B0909u);
@@ -468,8 +478,16 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const bf16* __
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             uint32_t km[2] = {~0u, ~0u};  // keep masks of queries q (qg 0) and q ^ 16 (qg 1): one hash
-            if constexpr (DROP)
+            if constexpr (DROP) {
+#if ATTN_BWD_MASK_PROBE
+              uint32_t wv = pre;
+              asm volatile("" : "+v"(wv));  // formed here, not hoisted (the hoisted masks spill)
+              km[0] = (uint32_t)__builtin_amdgcn_sbfe((int)wv, (4 * fi + r) & 31, 1);
+              km[1] = (uint32_t)__builtin_amdgcn_sbfe((int)wv, (4 * fi + r + 16) & 31, 1);
+#else
               drop_keep_masks(tk2, drop_fin(pre + (uint32_t)(16 * fi + r) * kDropC1, seed_kx(seed)), km[0], km[1]);
+#endif
+            }
 #pragma unroll
             for (int qg = 0; qg < 2; ++qg) {
               float p = __builtin_amdgcn_exp2f(fmaf(s[qg][fi][r], sl2, -lse2[qg]));
@@ -627,9 +645,17 @@ __global__ __launch_bounds__(64 * kDkdvWaves) __attribute__((amdgpu_waves_per_eu
             for (int r = 0; r < 4; ++r) {
               uint32_t km[2] = {~0u, ~0u};  // queries q and q^16 (fl = 0, 1) share one dropout hash
               // counter (bh*T + q0 + 4g + 32hq + r) * T + key: a lane base plus (32hq + r) * T + 16kg (uniform)
-              if constexpr (DROP)
+              if constexpr (DROP) {
+#if ATTN_BWD_MASK_PROBE
+                uint32_t wv = pre_t;
+                asm volatile("" : "+v"(wv));
+                km[0] = (uint32_t)__builtin_amdgcn_sbfe((int)wv, (8 * hq + 2 * r + kg) & 31, 1);
+                km[1] = (uint32_t)__builtin_amdgcn_sbfe((int)wv, (8 * hq + 2 * r + kg + 16) & 31, 1);
+#else
                 drop_keep_masks(tk2, drop_fin(pre_t + ((uint32_t)(32 * hq + r) * (uint32_t)T + 16u * kg) * kDropC1,
                                               seed_kx(seed)), km[0], km[1]);
+#endif
+              }
 #pragma unroll
               for (int fl = 0; fl < 2; ++fl) {
                 float p = __builtin_amdgcn_exp2f(fmaf(s[kg][fl][r], sl2, -l4[fl][r]));
