@@ -118,6 +118,67 @@ __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ src
     dst[i] = st_v<TD>(i < n ? src[i] : 0.f);
 }
 
+// 8 consecutive elements as fp32 (one 16-B load of bf16, two of fp32) / stored from fp32 (16-B stores). The FSDP
+// passes below run on them where every pointer is 16-B aligned (the flat units are): the per-element 2-B accesses ran
+// at 2-3 TB/s (profiles/r4f/summary_fsdp.txt: unpack 31 us for a 7.1 M-parameter block)
+template <typename T>
+__device__ __forceinline__ void ld8(const T* p, float (&v)[8]) {
+  if constexpr (sizeof(T) == 2) {
+    const bf16x8 x = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = bf2f(x[e]);
+  } else {
+    const f32x4 a = reinterpret_cast<const f32x4*>(p)[0], b = reinterpret_cast<const f32x4*>(p)[1];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = a[e], v[4 + e] = b[e];
+  }
+}
+template <typename T>
+__device__ __forceinline__ void st8(T* p, const float (&v)[8]) {
+  if constexpr (sizeof(T) == 2) {
+    bf16x8 x;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) x[e] = f2bf(v[e]);
+    *reinterpret_cast<bf16x8*>(p) = x;
+  } else {
+    reinterpret_cast<f32x4*>(p)[0] = f32x4{v[0], v[1], v[2], v[3]};
+    reinterpret_cast<f32x4*>(p)[1] = f32x4{v[4], v[5], v[6], v[7]};
+  }
+}
+template <typename TS>
+__global__ __launch_bounds__(256) void unpack8_kernel(const TS* __restrict__ src, float* __restrict__ dst,
+                                                      bf16* __restrict__ dst_bf, size_t n8) {
+  for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < n8; i += (size_t)gridDim.x * 256) {
+    float v[8];
+    ld8(src + 8 * i, v);
+    if (dst) st8(dst + 8 * i, v);
+    if (dst_bf) st8(dst_bf + 8 * i, v);
+  }
+}
+template <typename TS>
+__global__ __launch_bounds__(256) void accum8_kernel(const TS* __restrict__ src, float* __restrict__ dst, size_t n8,
+                                                     int accumulate) {
+  for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < n8; i += (size_t)gridDim.x * 256) {
+    float v[8], d[8];
+    ld8(src + 8 * i, v);
+    if (accumulate) {
+      ld8(dst + 8 * i, d);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = d[e] + v[e];
+    }
+    st8(dst + 8 * i, v);
+  }
+}
+template <typename TD>
+__global__ __launch_bounds__(256) void pack8_kernel(const float* __restrict__ src, TD* __restrict__ dst, size_t n8) {
+  for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < n8; i += (size_t)gridDim.x * 256) {
+    float v[8];
+    ld8(src + 8 * i, v);
+    st8(dst + 8 * i, v);
+  }
+}
+bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
 int grid_for(size_t n) {
   const size_t g = (n + 255) / 256;
   return (int)(g > 4096 ? 4096 : (g == 0 ? 1 : g));
@@ -180,13 +241,37 @@ GPT2MI_EXPORT int gpt2mi_scale_f32(float* x, size_t n, float s, void* stream) {
   return gpt2mi::check_launch("scale_f32");
 }
 
+// The FSDP passes: 8 elements per lane over the 16-B aligned prefix of multiples of 8, the element kernels over the
+// rest (and over everything when a pointer is not 16-B aligned)
+template <typename TS>
+static void unpack_t(const TS* src, float* dst, bf16* dst_bf, size_t n, hipStream_t s) {
+  const size_t n8 = al16(src) && al16(dst) && al16(dst_bf) ? n / 8 : 0;
+  if (n8) unpack8_kernel<TS><<<grid_for(n8), 256, 0, s>>>(src, dst, dst_bf, n8);
+  if (n > 8 * n8)
+    unpack_kernel<TS><<<grid_for(n - 8 * n8), 256, 0, s>>>(src + 8 * n8, dst ? dst + 8 * n8 : nullptr,
+                                                          dst_bf ? dst_bf + 8 * n8 : nullptr, n - 8 * n8);
+}
+template <typename TS>
+static void accum_t(const TS* src, float* dst, size_t n, int accumulate, hipStream_t s) {
+  const size_t n8 = al16(src) && al16(dst) ? n / 8 : 0;
+  if (n8) accum8_kernel<TS><<<grid_for(n8), 256, 0, s>>>(src, dst, n8, accumulate);
+  if (n > 8 * n8) accum_kernel<TS><<<grid_for(n - 8 * n8), 256, 0, s>>>(src + 8 * n8, dst + 8 * n8, n - 8 * n8, accumulate);
+}
+template <typename TD>
+static void pack_t(const float* src, TD* dst, size_t n, size_t n_pad, hipStream_t s) {
+  const size_t n8 = al16(src) && al16(dst) ? n / 8 : 0;
+  if (n8) pack8_kernel<TD><<<grid_for(n8), 256, 0, s>>>(src, dst, n8);
+  if (n_pad > 8 * n8)
+    pack_kernel<TD><<<grid_for(n_pad - 8 * n8), 256, 0, s>>>(src + 8 * n8, dst + 8 * n8, n - 8 * n8, n_pad - 8 * n8);
+}
+
 GPT2MI_EXPORT int gpt2mi_fsdp_unpack(const void* src, int src_f32, float* dst_f32, uint16_t* dst_bf16, size_t n,
                                      void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (src_f32)
-    unpack_kernel<float><<<grid_for(n), 256, 0, s>>>((const float*)src, dst_f32, (bf16*)dst_bf16, n);
+    unpack_t<float>((const float*)src, dst_f32, (bf16*)dst_bf16, n, s);
   else
-    unpack_kernel<bf16><<<grid_for(n), 256, 0, s>>>((const bf16*)src, dst_f32, (bf16*)dst_bf16, n);
+    unpack_t<bf16>((const bf16*)src, dst_f32, (bf16*)dst_bf16, n, s);
   return gpt2mi::check_launch("fsdp_unpack");
 }
 
@@ -194,17 +279,17 @@ GPT2MI_EXPORT int gpt2mi_fsdp_pack(const float* src, void* dst, int dst_f32, siz
   GPT2MI_REQUIRE(n_pad >= n, "fsdp_pack: n_pad=%zu < n=%zu", n_pad, n);
   hipStream_t s = (hipStream_t)stream;
   if (dst_f32)
-    pack_kernel<float><<<grid_for(n_pad), 256, 0, s>>>(src, (float*)dst, n, n_pad);
+    pack_t<float>(src, (float*)dst, n, n_pad, s);
   else
-    pack_kernel<bf16><<<grid_for(n_pad), 256, 0, s>>>(src, (bf16*)dst, n, n_pad);
+    pack_t<bf16>(src, (bf16*)dst, n, n_pad, s);
   return gpt2mi::check_launch("fsdp_pack");
 }
 
 GPT2MI_EXPORT int gpt2mi_fsdp_accum(const void* src, int src_f32, float* dst, size_t n, int accumulate, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (src_f32)
-    accum_kernel<float><<<grid_for(n), 256, 0, s>>>((const float*)src, dst, n, accumulate);
+    accum_t<float>((const float*)src, dst, n, accumulate, s);
   else
-    accum_kernel<bf16><<<grid_for(n), 256, 0, s>>>((const bf16*)src, dst, n, accumulate);
+    accum_t<bf16>((const bf16*)src, dst, n, accumulate, s);
   return gpt2mi::check_launch("fsdp_accum");
 }

@@ -893,3 +893,34 @@ def test_wgrad_slab_precision_per_element_at_the_proj_shape():
     from gpt_2_distributed_amd.engine import Engine
     default = "bf16_slabs" if Engine.WGRAD_BF16_SLABS else "fp32_slabs"
     assert stats[default]["worst_band"] <= bound, (default, stats)
+
+
+@pytest.mark.parametrize("n,off", [(1000, 0), (1003, 0), (7_087_872, 0), (4099, 1), (4099, 3)])
+def test_fsdp_pack_unpack_accum(n, off):
+    """FSDP's flat-unit passes (aux_ops.hip): 8 elements per lane over the 16-B aligned prefix, the element kernels
+    over the tail or for unaligned pointers (off = an element offset into the buffers); exactly torch's casts
+    (RNE to bf16) and fp32 adds."""
+    g = torch.Generator().manual_seed(n + off)
+    x = torch.randn(n + off, generator=g).to(dev)
+    for dt in (torch.bfloat16, torch.float32):
+        # pack: fp32 grad range -> dt, zero-padded to n_pad
+        n_pad = n + 37
+        packed = torch.full((n_pad + off,), 7.0, dtype=dt, device=dev)
+        L().fsdp_pack(x[off:], packed[off:], n, n_pad)
+        torch.cuda.synchronize()
+        assert torch.equal(packed[off:off + n], x[off:].to(dt)) and bool((packed[off + n:] == 0).all())
+        # unpack: dt -> fp32 + bf16 views
+        f32 = torch.empty(n + off, device=dev)
+        b16 = torch.empty(n + off, dtype=torch.bfloat16, device=dev)
+        L().fsdp_unpack(packed[off:], f32[off:], b16[off:], n)
+        torch.cuda.synchronize()
+        assert torch.equal(f32[off:], packed[off:off + n].float())
+        assert torch.equal(b16[off:], packed[off:off + n].float().to(torch.bfloat16))
+        # accum: dst (+)= src
+        base = torch.randn(n + off, generator=g).to(dev)
+        for acc in (True, False):
+            d = base.clone()
+            L().fsdp_accum(packed[off:], d[off:], n, accumulate=acc)
+            torch.cuda.synchronize()
+            exp = (base[off:] if acc else 0.0) + packed[off:off + n].float()
+            assert torch.equal(d[off:], exp)
