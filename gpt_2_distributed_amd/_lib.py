@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("GPT2MI_LIB") or os.path.join(_HERE, "libgpt2mi.so")
 
 # the ABI these bindings are written against (include/gpt2mi.h GPT2MI_ABI_VERSION): a stale or foreign
 # library is refused at load instead of being called with the wrong argument lists
-ABI_VERSION = 12
+ABI_VERSION = 11
 
 _c_int, _c_float, _c_size, _c_u64, _p = ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_void_p
 
@@ -33,8 +33,8 @@ _SIGS = {
     "gpt2mi_colsum_bf16": [_p, _p, _c_int, _c_int, _c_int, _p],
     "gpt2mi_gemm": [_c_int, _c_int, _c_int, _c_int, _c_int, _p, _c_int, _p, _c_int, _p, _c_int, _p, _p, _p, _c_int,
                     _c_float, _p, _c_int, _c_int, _c_float, _c_u64, _p, _c_int, _p],
-    "gpt2mi_attn_fwd": [_p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_float, _c_u64, _p, _p],
-    "gpt2mi_attn_bwd": [_p, _p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_float, _c_u64, _p, _p],
+    "gpt2mi_attn_fwd": [_p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_float, _c_u64, _p],
+    "gpt2mi_attn_bwd": [_p, _p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_float, _c_u64, _p],
     "gpt2mi_xent_fwd": [_p, _c_int, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _p, _p, _p],
     "gpt2mi_adamw": [_p, _p, _p, _p, _p, _c_size, _c_float, _c_float, _c_float, _c_float, _c_float, _c_int,
                      _c_float, _p, _p, _p],
@@ -216,37 +216,14 @@ def wgrad_splits(M, N, K, cus=256):
     return best
 
 
-def drop_bits_words(B, T, H):
-    """Size (int32 words) of the attention keep-bit buffer of one layer (gpt2mi.h gpt2mi_attn_fwd drop_bits)."""
-    return B * H * T * T // 32
+def attn_fwd(qkv, out, lse, B, T, H, D, p_drop=0.0, seed=0):
+    _call("gpt2mi_attn_fwd_f32" if _f32(qkv) else "gpt2mi_attn_fwd", _ptr(qkv), _ptr(out), _ptr(lse), B, T, H, D, p_drop, seed, _stream())
 
 
-def attn_fwd(qkv, out, lse, B, T, H, D, p_drop=0.0, seed=0, drop_bits=None):
-    """drop_bits: optional int32 [drop_bits_words(B, T, H)] receiving the dropout keep decisions (bf16 path)."""
-    if _f32(qkv):
-        _call("gpt2mi_attn_fwd_f32", _ptr(qkv), _ptr(out), _ptr(lse), B, T, H, D, p_drop, seed, _stream())
-    else:
-        _check_bits(drop_bits, B, T, H)
-        _call("gpt2mi_attn_fwd", _ptr(qkv), _ptr(out), _ptr(lse), B, T, H, D, p_drop, seed, _ptr(drop_bits), _stream())
-
-
-def attn_bwd(qkv, out, dout, lse, delta, dqkv, B, T, H, D, p_drop=0.0, seed=0, colsum=None, drop_bits=None):
-    """colsum: optional fp32 [B*T/32, 3C] partial column sums of dqkv (bf16 path; sum rows with colsum_bf16).
-    drop_bits: the buffer attn_fwd filled with the same qkv / p_drop / seed (None: the masks are hashed again)."""
-    if _f32(qkv):
-        _call("gpt2mi_attn_bwd_f32", _ptr(qkv), _ptr(out), _ptr(dout), _ptr(lse), _ptr(delta), _ptr(dqkv),
-              _ptr(colsum), B, T, H, D, p_drop, seed, _stream())
-    else:
-        _check_bits(drop_bits, B, T, H)
-        _call("gpt2mi_attn_bwd", _ptr(qkv), _ptr(out), _ptr(dout), _ptr(lse), _ptr(delta), _ptr(dqkv), _ptr(colsum),
-              B, T, H, D, p_drop, seed, _ptr(drop_bits), _stream())
-
-
-def _check_bits(bits, B, T, H):
-    if bits is not None and (bits.dtype != torch.int32 or not bits.is_contiguous()
-                             or bits.numel() < drop_bits_words(B, T, H) or bits.data_ptr() % 16):
-        raise ValueError(f"drop_bits: need a contiguous 16-B aligned int32 tensor of >= {drop_bits_words(B, T, H)} "
-                         "words")
+def attn_bwd(qkv, out, dout, lse, delta, dqkv, B, T, H, D, p_drop=0.0, seed=0, colsum=None):
+    """colsum: optional fp32 [B*T/32, 3C] partial column sums of dqkv (bf16 path; sum rows with colsum_bf16)."""
+    _call("gpt2mi_attn_bwd_f32" if _f32(qkv) else "gpt2mi_attn_bwd", _ptr(qkv), _ptr(out), _ptr(dout), _ptr(lse),
+          _ptr(delta), _ptr(dqkv), _ptr(colsum), B, T, H, D, p_drop, seed, _stream())
 
 
 def xent_fwd(logits, ld, labels, loss_rows, lse, dlogits, ldd, M, V, loss, inv_count, ignore_index=-100):

@@ -46,12 +46,6 @@ GPT2MI_PRODUCT_KNOB(ATTN_FWD_OCC, 3);
 GPT2MI_PRODUCT_KNOB(ATTN_FWD_LMAX, 1);
 GPT2MI_PRODUCT_KNOB(ATTN_DKDV_SB, 1);
 GPT2MI_PRODUCT_KNOB(ATTN_DKDV_WAVES, 4);
-// A/B probe only (WRONG masks): the keep masks from bit-field extracts / shifts of a per-tile word instead of the counter
-// hash, pricing kernels that read precomputed mask bits
-#ifndef ATTN_BWD_MASK_PROBE
-#define ATTN_BWD_MASK_PROBE 0
-#endif
-GPT2MI_PRODUCT_KNOB(ATTN_BWD_MASK_PROBE, 0);
 constexpr int kDkdvWaves = ATTN_DKDV_WAVES;  // waves per dK/dV workgroup (32 keys each)
 constexpr int BKB = 32 * kDkdvWaves;        // keys per workgroup in dK/dV
 constexpr int BQT = 64;  // queries per Q/dO tile in dK/dV
@@ -202,22 +196,11 @@ __device__ __forceinline__ void attn_block(int& bh, int& blk) {
 
 // Dropout of attention probability (q, key) of head bh: 16-bit half (q >> 4) & 1 of
 // drop_hash(seed, (bh*T + (q & ~16))*T + key) — queries q and q^16 of one key share a hash.
-//
-// Keep bits (BITS, ABI v12): the forward also stores every decision it draws, one 32-bit word per lane of a
-// (32-query, 64-key) wave tile, so the backward reads them instead of hashing again. Word (bh, q >> 5, key >> 6, lane
-// 16 g + i) holds the 32 decisions of forward lane (g, i): query (q & ~31) + 16 qg + i and keys (key & ~63) + 16 fi +
-// 4 g + r at bit 16 qg + 4 fi + r. dQ reads its own word per key tile (the forward's lane map); dK/dV, whose lanes hold
-// the transposed map (query 4 g + r, key i), reads the 4 words of forward lanes (i >> 2) * 16 + 4 g + r (r = 0..3) of
-// each 32-query half as one 16-B load.
-__device__ __forceinline__ size_t bits_word(int bh, int T, int q, int key) {
-  return (((size_t)bh * (T >> 5) + (q >> 5)) * (T >> 6) + (key >> 6)) * 64;
-}
 
 // ---------------------------------------------------------------------------------------------
-template <bool DROP, bool BITS>
+template <bool DROP>
 __global__ __launch_bounds__(kThreads, ATTN_FWD_OCC) void attn_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
-                                                               float* __restrict__ lse, uint32_t* __restrict__ dbits,
-                                                               int T, int H, float scale,
+                                                               float* __restrict__ lse, int T, int H, float scale,
                                                                uint64_t seed, uint32_t thr, float inv_keep) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * BKV * 128];  // 2 stages x (K, V)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
@@ -335,7 +318,7 @@ __global__ __launch_bounds__(kThreads, ATTN_FWD_OCC) void attn_fwd_kernel(const 
       // P packed to bf16 once per 32-key half (kk): the row sums (before dropout: the normaliser is the undropped
       // softmax denominator) and P.V read the same fragments. Dropout on the packed P (its 1/(1-p) goes into the
       // final scale): one hash per (q, q^16) pair of a key, both decisions from one packed int16 subtract.
-      [[maybe_unused]] uint32_t pre = 0, tk2 = 0, wb = 0;
+      [[maybe_unused]] uint32_t pre = 0, tk2 = 0;
       if constexpr (DROP) {
         pre = drop_pre(seed32(seed), ((uint32_t)bh * T + q_lo + (lane & 15)) * (uint32_t)T + k_lo + 4 * g);
         tk2 = drop_tk2(thr);
@@ -350,20 +333,11 @@ __global__ __launch_bounds__(kThreads, ATTN_FWD_OCC) void attn_fwd_kernel(const 
 #pragma unroll
           for (int d = 0; d < 4; ++d) {  // dword d: keys (fi, r), (fi, r + 1) with fi = 2kk + (d >> 1), r = 2(d & 1)
             const uint32_t c = 16 * (2 * kk + (d >> 1)) + 2 * (d & 1);
-#if ATTN_BWD_MASK_PROBE
-            const uint32_t ka = pre << (c & 15), kb = pre << ((c + 1) & 15);
-#else
             const uint32_t ka = drop_keep_mask2(tk2, drop_fin(pre + c * kDropC1, seed_kx(seed)));
             const uint32_t kb = drop_keep_mask2(tk2, drop_fin(pre + (c + 1) * kDropC1, seed_kx(seed)));
-#endif
             // the bytes of each bf16 = the sign (keep bit) of key r's / key r+1's decision for query group 0 / 1
             w0[d] &= __builtin_amdgcn_perm(kb, ka, 0x0A0A0808u);
             w1[d] &= __builtin_amdgcn_perm(kb, ka, 0x0B0B0909u);
-            if constexpr (BITS) {  // keep bits 15 / 31 (query group 0 / 1) of keys (fi, r), (fi, r + 1) -> bits p, 16 + p
-              const int pb = 4 * (2 * kk + (d >> 1)) + 2 * (d & 1);
-              wb |= (ka >> (15 - pb)) & ((1u << pb) | (1u << (16 + pb)));
-              wb |= (kb >> (14 - pb)) & ((2u << pb) | (2u << (16 + pb)));
-            }
           }
           p0 = __builtin_bit_cast(bf16x8, w0);
           p1 = __builtin_bit_cast(bf16x8, w1);
@@ -375,7 +349,6 @@ __global__ __launch_bounds__(kThreads, ATTN_FWD_OCC) void attn_fwd_kernel(const 
           o[1][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vt, p1, o[1][fd], 0, 0, 0);
         }
       }
-      if constexpr (DROP && BITS) dbits[bits_word(bh, T, q_lo, k_lo) + lane] = wb;
     }
     __syncthreads();
   }
@@ -395,12 +368,11 @@ __global__ __launch_bounds__(kThreads, ATTN_FWD_OCC) void attn_fwd_kernel(const 
 // dQ: query-outer; recomputes P from the saved LSE. dS^T = P^T o (dP^T - delta), dQ^T += K^T dS^T.
 // delta = rowsum(dO o O) of the wave's own queries is formed here (no separate pass) and written out for
 // the dK/dV kernel, which runs after this one.
-template <bool DROP, bool BITS>
+template <bool DROP>
 __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const bf16* __restrict__ qkv,
                                                                   const bf16* __restrict__ out,
                                                                   const bf16* __restrict__ dout,
                                                                   const float* __restrict__ lse,
-                                                                  const uint32_t* __restrict__ dbits,
                                                                   float* __restrict__ delta,
                                                                   bf16* __restrict__ dqkv, float* __restrict__ csum,
                                                                   int T, int H, float scale, uint64_t seed,
@@ -459,20 +431,13 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const bf16* __
     const int cur = j & 1;
     const char* Ks = smem + cur * 2 * BKV * 128;
     const char* Vs = Ks + BKV * 128;
-    const int k_lo = j * BKV;
-    const bool active = wave_valid && k_lo <= q_lo + 31;
-    // BITS: this lane's keep word of the tile (the forward wrote exactly the tiles this loop visits), loaded ahead of
-    // the next tile's DMAs so that its wait does not cover them
-    [[maybe_unused]] uint32_t wb = 0u;
-    if constexpr (DROP && BITS) {
-      if (active) wb = dbits[bits_word(bh, T, q_lo, k_lo) + lane];
-    }
     if (j + 1 < nkv) {  // next K/V tile by LDS-DMA into the stage released by tile j-1's barrier
       char* nxt = smem + (cur ^ 1) * 2 * BKV * 128;
       tile_dma(nxt, rs, (j + 1) * BKV, C + h * D, (int)ld, loff, wu);
       tile_dma(nxt + BKV * 128, rs, (j + 1) * BKV, 2 * C + h * D, (int)ld, loff, wu);
     }
-    if (active) {
+    const int k_lo = j * BKV;
+    if (wave_valid && k_lo <= q_lo + 31) {
       const bool diag = k_lo + BKV - 1 > q_lo;
       f32x4 s[2][4], dp[2][4];
 #pragma unroll
@@ -496,28 +461,15 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const bf16* __
       auto elementwise = [&](auto diag_c) {
         constexpr bool DIAG = decltype(diag_c)::value;
         uint32_t pre = 0;
-        if constexpr (DROP && !BITS)
+        if constexpr (DROP)
           pre = drop_pre(seed32(seed), ((uint32_t)bh * T + q_lo + (lane & 15)) * (uint32_t)T + k_lo + 4 * g);
 #pragma unroll
         for (int fi = 0; fi < 4; ++fi)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             uint32_t km[2] = {~0u, ~0u};  // keep masks of queries q (qg 0) and q ^ 16 (qg 1): one hash
-            if constexpr (DROP && BITS) {
-              uint32_t wv = wb;
-              asm volatile("" : "+v"(wv));  // extracted here: hoisted, the 32 masks of a tile spill
-              km[0] = (uint32_t)__builtin_amdgcn_sbfe((int)wv, 4 * fi + r, 1);
-              km[1] = (uint32_t)__builtin_amdgcn_sbfe((int)wv, 16 + 4 * fi + r, 1);
-            } else if constexpr (DROP) {
-#if ATTN_BWD_MASK_PROBE
-              uint32_t wv = pre;
-              asm volatile("" : "+v"(wv));  // formed here, not hoisted (the hoisted masks spill)
-              km[0] = (uint32_t)__builtin_amdgcn_sbfe((int)wv, (4 * fi + r) & 31, 1);
-              km[1] = (uint32_t)__builtin_amdgcn_sbfe((int)wv, (4 * fi + r + 16) & 31, 1);
-#else
+            if constexpr (DROP)
               drop_keep_masks(tk2, drop_fin(pre + (uint32_t)(16 * fi + r) * kDropC1, seed_kx(seed)), km[0], km[1]);
-#endif
-            }
 #pragma unroll
             for (int qg = 0; qg < 2; ++qg) {
               float p = __builtin_amdgcn_exp2f(fmaf(s[qg][fi][r], sl2, -lse2[qg]));
@@ -558,11 +510,10 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const bf16* __
 
 // ---------------------------------------------------------------------------------------------
 // dK, dV: key-outer (128 keys per workgroup, 32 per wave) over 64-query tiles at or after the keys.
-template <bool DROP, bool BITS>
+template <bool DROP>
 __global__ __launch_bounds__(64 * kDkdvWaves) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_bwd_dkdv_kernel(const bf16* __restrict__ qkv,
                                                                     const bf16* __restrict__ dout,
                                                                     const float* __restrict__ lse,
-                                                                    const uint32_t* __restrict__ dbits,
                                                                     const float* __restrict__ delta,
                                                                     bf16* __restrict__ dqkv, float* __restrict__ csum,
                                                                     int T, int H, float scale, uint64_t seed,
@@ -632,23 +583,11 @@ __global__ __launch_bounds__(64 * kDkdvWaves) __attribute__((amdgpu_waves_per_eu
     const char* Ds = Qs + kTile;
     const float* Ls = reinterpret_cast<const float*>(Qs + 2 * kTile);
     const float* Dl = Ls + BQT;
-    const int q0 = i * BQT;
-    const bool active = wave_valid && q0 + BQT - 1 >= k_lo;  // wave-uniform: a query of the tile sees a key of the wave
-    // BITS: the forward's keep words of forward lanes (i >> 2) * 16 + 4g + r, r = 0..3, in each 32-query half (issued
-    // ahead of the next tile's loads, so that their wait does not cover those). A half the forward never visited (all
-    // its queries before the wave's keys) reads stale words: its entries are causally masked to P = 0, dS = 0 anyway.
-    [[maybe_unused]] u32x4 wq[2];
-    if constexpr (DROP && BITS) {
-      if (active) {
-        const size_t wo = (size_t)(((lane & 15) >> 2) * 16 + 4 * g);
-        wq[0] = *reinterpret_cast<const u32x4*>(dbits + bits_word(bh, T, q0, k_lo) + wo);
-        wq[1] = *reinterpret_cast<const u32x4*>(dbits + bits_word(bh, T, q0 + 32, k_lo) + wo);
-      }
-    }
     if (i + 1 < nqt) gload(i + 1, smem + (cur ^ 1) * kStage);
-    if (active) {
+    const int q0 = i * BQT;
+    if (wave_valid && q0 + BQT - 1 >= k_lo) {  // wave-uniform: a query of the tile sees a key of the wave
       const bool diag = q0 < k_lo + 31;
-      const uint32_t pre_t = (DROP && !BITS) ? drop_pre(seed32(seed), ((uint32_t)bh * T + q0 + 4 * g) * (uint32_t)T + k_lo + (lane & 15)) : 0u;
+      const uint32_t pre_t = DROP ? drop_pre(seed32(seed), ((uint32_t)bh * T + q0 + 4 * g) * (uint32_t)T + k_lo + (lane & 15)) : 0u;
       // Two 32-query halves per 64-query tile; each half is exactly one MFMA k-step of the dV/dK
       // products, so only half of S / dP is live at a time (register pressure -> occupancy).
 #pragma unroll
@@ -679,14 +618,6 @@ __global__ __launch_bounds__(64 * kDkdvWaves) __attribute__((amdgpu_waves_per_eu
         }
         // P = exp2(S*scale*log2e - LSE*log2e); dropped entries: P_drop = 0 (dV; its 1/(1-p) is applied
         // to dV at the end) and dP = 0 (dS); dP already carries 1/(1-p) through the prescaled V.
-        // BITS: the half's 4 words shifted so that bit 16 fl + 4 (fi0 + kg) is this lane's (fi0 = the wave's 32 keys
-        // within the forward's 64-key tile)
-        [[maybe_unused]] u32x4 wsh;
-        [[maybe_unused]] const int fb = (k_lo & 63) >> 2;
-        if constexpr (DROP && BITS) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) wsh[r] = wq[hq][r] >> (lane & 3);
-        }
         auto elementwise = [&](auto diag_c) {
           constexpr bool DIAG = decltype(diag_c)::value;
 #pragma unroll
@@ -696,20 +627,9 @@ __global__ __launch_bounds__(64 * kDkdvWaves) __attribute__((amdgpu_waves_per_eu
             for (int r = 0; r < 4; ++r) {
               uint32_t km[2] = {~0u, ~0u};  // queries q and q^16 (fl = 0, 1) share one dropout hash
               // counter (bh*T + q0 + 4g + 32hq + r) * T + key: a lane base plus (32hq + r) * T + 16kg (uniform)
-              if constexpr (DROP && BITS) {
-                km[0] = (uint32_t)__builtin_amdgcn_sbfe((int)wsh[r], fb + 4 * kg, 1);
-                km[1] = (uint32_t)__builtin_amdgcn_sbfe((int)wsh[r], 16 + fb + 4 * kg, 1);
-              } else if constexpr (DROP) {
-#if ATTN_BWD_MASK_PROBE
-                uint32_t wv = pre_t;
-                asm volatile("" : "+v"(wv));
-                km[0] = (uint32_t)__builtin_amdgcn_sbfe((int)wv, (8 * hq + 2 * r + kg) & 31, 1);
-                km[1] = (uint32_t)__builtin_amdgcn_sbfe((int)wv, (8 * hq + 2 * r + kg + 16) & 31, 1);
-#else
+              if constexpr (DROP)
                 drop_keep_masks(tk2, drop_fin(pre_t + ((uint32_t)(32 * hq + r) * (uint32_t)T + 16u * kg) * kDropC1,
                                               seed_kx(seed)), km[0], km[1]);
-#endif
-              }
 #pragma unroll
               for (int fl = 0; fl < 2; ++fl) {
                 float p = __builtin_amdgcn_exp2f(fmaf(s[kg][fl][r], sl2, -l4[fl][r]));
@@ -768,67 +688,55 @@ __global__ __launch_bounds__(64 * kDkdvWaves) __attribute__((amdgpu_waves_per_eu
 }  // namespace
 
 GPT2MI_EXPORT int gpt2mi_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int T, int H, int head_dim,
-                                  float p_drop, uint64_t seed, uint32_t* drop_bits, void* stream) {
+                                  float p_drop, uint64_t seed, void* stream) {
   GPT2MI_REQUIRE(head_dim == D, "attn_fwd: head_dim=%d (only 64 is built)", head_dim);
   GPT2MI_REQUIRE(p_drop <= 0.f || (size_t)B * H * T * T < (1ull << 32),
                  "attn_fwd: B*H*T*T exceeds the 32-bit dropout hash index");
   GPT2MI_REQUIRE(T % 64 == 0 && T > 0, "attn_fwd: T=%d must be a multiple of 64", T);
   GPT2MI_REQUIRE((size_t)T * 3 * H * D * sizeof(bf16) < (1ull << 31),
                  "attn_fwd: T*3C too large for the 32-bit buffer offsets of one batch row (T=%d)", T);
-  GPT2MI_REQUIRE(((uintptr_t)drop_bits & 15) == 0, "attn_fwd: drop_bits must be 16-byte aligned");
   const float scale = 1.f / sqrtf((float)head_dim);
   dim3 grid((T + BQ - 1) / BQ, B * H);
   const uint32_t thr = drop_threshold(p_drop);
   const float ik = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
-  hipStream_t s = (hipStream_t)stream;
-  const bf16* q = (const bf16*)qkv;
-  if (thr && drop_bits)
-    attn_fwd_kernel<true, true><<<grid, kThreads, 0, s>>>(q, (bf16*)out, lse, drop_bits, T, H, scale, seed, thr, ik);
-  else if (thr)
-    attn_fwd_kernel<true, false><<<grid, kThreads, 0, s>>>(q, (bf16*)out, lse, nullptr, T, H, scale, seed, thr, ik);
+  if (thr)
+    attn_fwd_kernel<true><<<grid, kThreads, 0, (hipStream_t)stream>>>((const bf16*)qkv, (bf16*)out, lse, T, H, scale,
+                                                                      seed, thr, ik);
   else
-    attn_fwd_kernel<false, false><<<grid, kThreads, 0, s>>>(q, (bf16*)out, lse, nullptr, T, H, scale, seed, thr, ik);
+    attn_fwd_kernel<false><<<grid, kThreads, 0, (hipStream_t)stream>>>((const bf16*)qkv, (bf16*)out, lse, T, H, scale,
+                                                                       seed, thr, ik);
   return gpt2mi::check_launch("attn_fwd");
 }
 
 GPT2MI_EXPORT int gpt2mi_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse,
                                   float* delta, uint16_t* dqkv, float* dqkv_colsum, int B, int T, int H,
-                                  int head_dim, float p_drop, uint64_t seed, const uint32_t* drop_bits, void* stream) {
+                                  int head_dim, float p_drop, uint64_t seed, void* stream) {
   GPT2MI_REQUIRE(head_dim == D, "attn_bwd: head_dim=%d (only 64 is built)", head_dim);
   GPT2MI_REQUIRE(p_drop <= 0.f || (size_t)B * H * T * T < (1ull << 32),
                  "attn_bwd: B*H*T*T exceeds the 32-bit dropout hash index");
   GPT2MI_REQUIRE(T % 64 == 0 && T > 0, "attn_bwd: T=%d must be a multiple of 64", T);
   GPT2MI_REQUIRE((size_t)T * 3 * H * D * sizeof(bf16) < (1ull << 31),
                  "attn_bwd: T*3C too large for the 32-bit buffer offsets of one batch row (T=%d)", T);
-  GPT2MI_REQUIRE(((uintptr_t)drop_bits & 15) == 0, "attn_bwd: drop_bits must be 16-byte aligned");
   hipStream_t s = (hipStream_t)stream;
   const float scale = 1.f / sqrtf((float)head_dim);
   const uint32_t thr = drop_threshold(p_drop);
   const float ik = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
-  const bf16 *q = (const bf16*)qkv, *o = (const bf16*)out, *dO = (const bf16*)dout;
   // dQ first: it forms delta (dO . O per query) for the dK/dV kernel
   const dim3 gq((T + BQ - 1) / BQ, B * H);
-  if (thr && drop_bits)
-    attn_bwd_dq_kernel<true, true><<<gq, kThreads, 0, s>>>(q, o, dO, lse, drop_bits, delta, (bf16*)dqkv, dqkv_colsum,
-                                                           T, H, scale, seed, thr, ik);
-  else if (thr)
-    attn_bwd_dq_kernel<true, false><<<gq, kThreads, 0, s>>>(q, o, dO, lse, nullptr, delta, (bf16*)dqkv, dqkv_colsum,
-                                                            T, H, scale, seed, thr, ik);
+  if (thr)
+    attn_bwd_dq_kernel<true><<<gq, kThreads, 0, s>>>((const bf16*)qkv, (const bf16*)out, (const bf16*)dout, lse, delta,
+                                                     (bf16*)dqkv, dqkv_colsum, T, H, scale, seed, thr, ik);
   else
-    attn_bwd_dq_kernel<false, false><<<gq, kThreads, 0, s>>>(q, o, dO, lse, nullptr, delta, (bf16*)dqkv, dqkv_colsum,
-                                                             T, H, scale, seed, thr, ik);
+    attn_bwd_dq_kernel<false><<<gq, kThreads, 0, s>>>((const bf16*)qkv, (const bf16*)out, (const bf16*)dout, lse,
+                                                      delta, (bf16*)dqkv, dqkv_colsum, T, H, scale, seed, thr, ik);
   int rc = gpt2mi::check_launch("attn_bwd_dq");
   if (rc) return rc;
   const dim3 gkv((T + BKB - 1) / BKB, B * H);
-  constexpr int nt = 64 * kDkdvWaves;
-  if (thr && drop_bits)
-    attn_bwd_dkdv_kernel<true, true><<<gkv, nt, 0, s>>>(q, dO, lse, drop_bits, delta, (bf16*)dqkv, dqkv_colsum, T, H,
-                                                        scale, seed, thr, ik);
-  else if (thr)
-    attn_bwd_dkdv_kernel<true, false><<<gkv, nt, 0, s>>>(q, dO, lse, nullptr, delta, (bf16*)dqkv, dqkv_colsum, T, H,
-                                                         scale, seed, thr, ik);
+  if (thr)
+    attn_bwd_dkdv_kernel<true><<<gkv, 64 * kDkdvWaves, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta,
+                                                        (bf16*)dqkv, dqkv_colsum, T, H, scale, seed, thr, ik);
   else
-    attn_bwd_dkdv_kernel<false, false><<<gkv, nt, 0, s>>>(q, dO, lse, nullptr, delta, (bf16*)dqkv, dqkv_colsum, T, H,
-                                                          scale, seed, thr, ik);
+    attn_bwd_dkdv_kernel<false><<<gkv, 64 * kDkdvWaves, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta,
+                                                         (bf16*)dqkv, dqkv_colsum, T, H, scale, seed, thr, ik);
   return gpt2mi::check_launch("attn_bwd_dkdv");
 }

@@ -122,10 +122,6 @@ class BlockActs:
     r2: torch.Tensor
     dgelu: torch.Tensor  # keep/(1-p) * gelu'(u) of the fc1 pre-activation u (from the fc1 epilogue)
     h: torch.Tensor
-    # the attention forward's dropout keep bits (bf16 path, p > 0; allocated at first use) and the (B, T, seed) of the
-    # forward that wrote them: the backward reads them only for that forward
-    dbits: Optional[torch.Tensor] = None
-    dbits_key: Optional[tuple] = None
 
     @staticmethod
     def alloc(cfg, B, T, device, act, xmid=True):
@@ -317,9 +313,6 @@ class Engine:
     # bf16 rounding per split leaves elements whose partial sums cancel with far larger relative errors
     # (tests/test_kernels_gpu.py::test_wgrad_slab_precision_per_element_at_the_proj_shape, 28 splits).
     WGRAD_BF16_SLABS = False
-    # The attention forward stores its dropout keep decisions (B*H*T^2/8 bytes per layer) and the backward reads them
-    # instead of hashing them again (gpt2mi.h gpt2mi_attn_fwd drop_bits; the same masks, bitwise equal gradients)
-    ATTN_DROP_BITS = True
     # Schedule flag added while a data-parallel wrapper's collective may run (GradHooks.inflight): since ABI v11
     # GPT2MI_SCHED_SHARED_CUS (the persistent GEMM takes its tiles from per-XCD work queues, gemm_pp.hip g_pp_queue);
     # v8-v10 passed GPT2MI_SCHED_NO_PERSISTENT (one tile per block) instead.
@@ -640,15 +633,8 @@ class Engine:
         pre = f"transformer.h.{l}."
         self._gemm(K.FWD, K.EPI_BF16, M, 3 * C, C, A.ln1, C, self.w(pre + "attn.qkv.weight", act), C, A.qkv, 3 * C,
                bias=self.p(pre + "attn.qkv.bias"))
-        bits = None
-        if self.ATTN_DROP_BITS and pa > 0 and act == BF16:
-            n = K.drop_bits_words(B, T, H)
-            if A.dbits is None or A.dbits.numel() < n:
-                A.dbits = torch.empty(n, dtype=torch.int32, device=self.device)
-            bits = A.dbits
-            A.dbits_key = (B, T, seeds[("attn", l)])
         with self._probe("attn_fwd"):
-            K.attn_fwd(A.qkv, A.ao, A.lse, B, T, H, C // H, pa, seeds[("attn", l)], drop_bits=bits)
+            K.attn_fwd(A.qkv, A.ao, A.lse, B, T, H, C // H, pa, seeds[("attn", l)])
         self._gemm(K.FWD, K.EPI_RESID, M, C, C, A.ao, C, self.w(pre + "attn.proj.weight", act), C, out, C,
                bias=self.p(pre + "attn.proj.bias"), resid=resid, p_drop=pr, seed=seeds[("proj", l)])
 
@@ -728,9 +714,8 @@ class Engine:
         pre = f"transformer.h.{l}."
         self._dgrad(act, M, dx_out, dY, pre + "attn.proj.weight", C, C)
         self._wgrad(S, act, C, C, M, dY, C, A.ao, C, self.g(pre + "attn.proj.weight"))
-        bits = A.dbits if (pa > 0 and act == BF16 and A.dbits_key == (B, T, seeds[("attn", l)])) else None
         K.attn_bwd(A.qkv, A.ao, dx_out, A.lse, S.delta, S.dqkv, B, T, H, C // H, pa, seeds[("attn", l)],
-                   colsum=S.dqkv_cs, drop_bits=bits)
+                   colsum=S.dqkv_cs)
         self._dgrad(act, M, dx_out, S.dqkv, pre + "attn.qkv.weight", C, 3 * C)
         self._wgrad(S, act, 3 * C, C, M, S.dqkv, 3 * C, A.ln1, C, self.g(pre + "attn.qkv.weight"))
         if S.dqkv_cs is not None:  # qkv bias grad: sum the attention backward's 32-token partials

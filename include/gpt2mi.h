@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GPT2MI_ABI_VERSION 12
+#define GPT2MI_ABI_VERSION 11
 
 const char* gpt2mi_last_error(void);
 int gpt2mi_abi_version(void); /* returns GPT2MI_ABI_VERSION of the built library */
@@ -113,19 +113,15 @@ int gpt2mi_gemm_wgrad_kt(int M, int N, int K, const uint16_t* A, int lda, const 
                          size_t workspace_floats, int splits, int sched, void* stream);
 
 /* K4-K8: causal flash attention, head_dim 64 — model.py:124-155. q/k/v read from qkv [B*T, 3C];
- * out [B*T, C] head-merged; lse [B*H, T] (natural log of the 1/sqrt(D)-scaled scores).
- * drop_bits (v12, may be NULL; used only when p_drop > 0): B*H*T*T/32 words (B*H*T^2/8 bytes, 16-B aligned) that
- * receive the forward's dropout keep decisions, for gpt2mi_attn_bwd to read instead of hashing them again. */
+ * out [B*T, C] head-merged; lse [B*H, T] (natural log of the 1/sqrt(D)-scaled scores). */
 int gpt2mi_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int T, int H, int head_dim, float p_drop,
-                    uint64_t seed, uint32_t* drop_bits, void* stream);
+                    uint64_t seed, void* stream);
 /* Backward: delta [B*H, T] workspace (dO.O, formed by the dQ pass); dqkv [B*T, 3C] written in the qkv
  * layout. dqkv_colsum (may be NULL): [B*T/32, 3C] fp32 partial column sums of the stored dqkv, one row
- * per 32 tokens — the qkv bias gradient after gpt2mi_colsum_f32 over its rows (model.py c_attn bias).
- * drop_bits (v12, may be NULL): the words gpt2mi_attn_fwd wrote with the same qkv, p_drop and seed (the same masks
- * as without them, bitwise equal gradients); NULL regenerates the masks from the hash. */
+ * per 32 tokens — the qkv bias gradient after gpt2mi_colsum_f32 over its rows (model.py c_attn bias). */
 int gpt2mi_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse, float* delta,
                     uint16_t* dqkv, float* dqkv_colsum, int B, int T, int H, int head_dim, float p_drop,
-                    uint64_t seed, const uint32_t* drop_bits, void* stream);
+                    uint64_t seed, void* stream);
 
 /* K13: F.cross_entropy(logits.view(-1,V), labels.view(-1), ignore_index) — model.py:357-359.
  * logits bf16 [M, ld]; writes loss_rows [M], lse [M], loss[0] = mean, inv_count[0] = 1/#valid and, if

@@ -48,9 +48,9 @@ def test_refuses_shapes_that_overflow_the_dropout_index():
     from gpt_2_distributed_amd import _lib
     lib = _lib.load()
     # attention: B*H*T*T = 256*16*1024*1024 = 2^32
-    assert lib.gpt2mi_attn_fwd(None, None, None, 256, 1024, 16, 64, 0.1, 1, None, None) == 22
+    assert lib.gpt2mi_attn_fwd(None, None, None, 256, 1024, 16, 64, 0.1, 1, None) == 22
     assert b"32-bit dropout" in lib.gpt2mi_last_error()
-    assert lib.gpt2mi_attn_bwd(None, None, None, None, None, None, None, 256, 1024, 16, 64, 0.1, 1, None, None) == 22
+    assert lib.gpt2mi_attn_bwd(None, None, None, None, None, None, None, 256, 1024, 16, 64, 0.1, 1, None) == 22
     # GEMM epilogue dropout: M*N = 2^20 * 2^13 = 2^33 pairs*2
     assert lib.gpt2mi_gemm(0, 2, 1 << 20, 1 << 13, 64, None, 64, None, 64, None, 1 << 13, None, None, None, 0,
                            1.0, None, 0, 1, 0.1, 1, None, 0, None) == 22

@@ -3,7 +3,6 @@ PyTorch fp32 reference of the same op on the same seeded inputs. Tolerances are 
 bf16 outputs are compared at bf16 resolution, fp32 outputs at accumulation-order resolution."""
 import math
 
-import numpy as np
 import pytest
 import torch
 
@@ -321,46 +320,6 @@ def test_attention_bwd_fused_bias_grad_partials(p):
     bias_grad = torch.zeros(3 * C, device=dev)
     L().colsum_bf16(cs, bias_grad, B * T // 32, 3 * C, 3 * C)
     assert rel_err(bias_grad.cpu(), d1.float().sum(0).cpu()) < 1e-5
-
-
-@pytest.mark.parametrize("B,T,H", [(1, 128, 2), (2, 192, 3), (1, 1024, 2), (4, 256, 2)])
-def test_attention_drop_bits(B, T, H):
-    """ABI v12 keep bits: the forward stores exactly the oracle's attention dropout decisions (oracle/dropout_ref.py
-    attn_scale, decoded through the word layout of attention.hip bits_word: word (bh, q >> 5, key >> 6, lane 16 g + i),
-    bit 16 qg + 4 fi + r) for every causal (q, key); writing them leaves the forward's outputs unchanged, and the
-    backward that reads them is bitwise equal to the one that hashes the masks again. T = 192: a partial query block
-    and dK/dV halves before the wave's keys (stale words, causally masked)."""
-    from oracle import dropout_ref
-    D, p, seed = 64, 0.1, (0x2545F491 << 32) | 12345
-    qkv, C = _attn_inputs(B, T, H, 31 * T + H)
-    qd = qkv.to(dev)
-    outs, bits = [], torch.full((L().drop_bits_words(B, T, H),), -1, dtype=torch.int32, device=dev)
-    lse = torch.empty(B * H, T, device=dev)
-    for db in (None, bits):
-        o = torch.empty(B * T, C, dtype=torch.bfloat16, device=dev)
-        L().attn_fwd(qd, o, lse, B, T, H, D, p, seed, drop_bits=db)
-        outs.append(o)
-    torch.cuda.synchronize()
-    assert torch.equal(outs[0], outs[1])
-    keep = dropout_ref.attn_scale(seed, B * H, T, p).numpy() > 0  # [BH, q, key]
-    w = bits.cpu().numpy().view(np.uint32)
-    bh, q, k = np.meshgrid(np.arange(B * H), np.arange(T), np.arange(T), indexing="ij")
-    word = (((bh * (T // 32) + q // 32) * (T // 64) + k // 64) * 64 + ((k >> 2) & 3) * 16 + (q & 15))
-    bit = 16 * ((q >> 4) & 1) + 4 * ((k & 63) >> 4) + (k & 3)
-    got = (w[word] >> bit.astype(np.uint32)) & 1
-    causal = k <= q
-    assert np.array_equal(got[causal].astype(bool), keep[causal])
-    dout = bf(torch.randn(B * T, C, generator=torch.Generator().manual_seed(T))).to(dev)
-    res = []
-    for db in (None, bits):
-        delta = torch.empty(B * H, T, device=dev)
-        dqkv = torch.empty(B * T, 3 * C, dtype=torch.bfloat16, device=dev)
-        cs = torch.empty(B * T // 32, 3 * C, device=dev)
-        L().attn_bwd(qd, outs[0], dout, lse, delta, dqkv, B, T, H, D, p, seed, colsum=cs, drop_bits=db)
-        res.append((delta, dqkv, cs))
-    torch.cuda.synchronize()
-    for a, b in zip(*res):
-        assert torch.equal(a, b)
 
 
 def test_attention_dropout_stats_and_grad_consistency():

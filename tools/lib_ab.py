@@ -25,12 +25,10 @@ def bind(path, _n=[0]):
     cp = os.path.join(tempfile.mkdtemp(), f"lib{_n[0]}.so")
     shutil.copy(path, cp)
     lib = ctypes.CDLL(cp)
-    lib.gpt2mi_abi_version.restype = ctypes.c_int
-    old = lib.gpt2mi_abi_version() < 12  # (v11 and before: no drop_bits argument before the stream)
     for name, args in K._SIGS.items():
         if hasattr(lib, name):
             fn = getattr(lib, name)
-            fn.argtypes = args[:-2] + args[-1:] if old and name in ("gpt2mi_attn_fwd", "gpt2mi_attn_bwd") else args
+            fn.argtypes = args
             fn.restype = K._RESTYPES.get(name, ctypes.c_int)
     return lib
 
@@ -180,35 +178,23 @@ def gemm_mode(libs, g, st):
 
 def attn_mode(libs, g, st):
     """LIB_AB_OP=attn: attention forward / backward at cfg 2 (B=64, T=1024, H=12, D=64, dropout 0.1); outputs
-    compared bitwise against the first library. ABI v12 libraries get the forward's keep-bit buffer unless
-    LIB_AB_BITS=0 (LIB_AB_BITS=0,1: per library)."""
+    compared bitwise against the first library."""
     B, T, H, D = 64, 1024, 12, 64
     C = H * D
     pd = float(os.environ.get("LIB_AB_PDROP", "0.1"))
     qkv = (torch.randn(B * T, 3 * C, device=dev, generator=g) * 0.5).to(torch.bfloat16)
     dout = (torch.randn(B * T, C, device=dev, generator=g) * 0.1).to(torch.bfloat16)
     res = []
-    use = [v != "0" for v in os.environ.get("LIB_AB_BITS", "1").split(",")]
-    use += [use[-1]] * len(libs)
-    for i, lib in enumerate(libs):
+    for lib in libs:
         out = torch.empty(B * T, C, dtype=torch.bfloat16, device=dev)
         lse = torch.empty(B * H * T, device=dev)
         delta = torch.empty(B * H * T, device=dev)
         dqkv = torch.empty(B * T, 3 * C, dtype=torch.bfloat16, device=dev)
-        v12 = lib.gpt2mi_abi_version() >= 12
-        bits = torch.empty(K.drop_bits_words(B, T, H), dtype=torch.int32, device=dev) if v12 and use[i] else None
-        res.append((out, lse, delta, dqkv, v12, bits))
-
-    def fwd(lib, r):
-        a = (qkv.data_ptr(), r[0].data_ptr(), r[1].data_ptr(), B, T, H, D, pd, 7)
-        return lib.gpt2mi_attn_fwd(*a, r[5].data_ptr() if r[5] is not None else None, st) if r[4] else \
-            lib.gpt2mi_attn_fwd(*a, st)
-
-    def bwd(lib, r):
-        a = (qkv.data_ptr(), r[0].data_ptr(), dout.data_ptr(), r[1].data_ptr(), r[2].data_ptr(), r[3].data_ptr(), None,
-             B, T, H, D, pd, 7)
-        return lib.gpt2mi_attn_bwd(*a, r[5].data_ptr() if r[5] is not None else None, st) if r[4] else \
-            lib.gpt2mi_attn_bwd(*a, st)
+        res.append((out, lse, delta, dqkv))
+    fwd = lambda lib, r: lib.gpt2mi_attn_fwd(qkv.data_ptr(), r[0].data_ptr(), r[1].data_ptr(), B, T, H, D, pd,  # noqa
+                                              7, st)
+    bwd = lambda lib, r: lib.gpt2mi_attn_bwd(qkv.data_ptr(), r[0].data_ptr(), dout.data_ptr(), r[1].data_ptr(),  # noqa
+                                              r[2].data_ptr(), r[3].data_ptr(), None, B, T, H, D, pd, 7, st)
     for lib, r in zip(libs, res):
         assert fwd(lib, r) == 0 and bwd(lib, r) == 0
     torch.cuda.synchronize()
