@@ -280,9 +280,11 @@ __device__ __forceinline__ void lds_barrier() {
 #endif
 
 // Persistent schedule: the work queue. Items (output tiles) are dealt to the 8 XCD labels (blockIdx % 8) in contiguous
-// ranges, as xcd_remap does; the first two items of every block are static (blockIdx / 8 and that plus the blocks per
-// label), every later one is taken from its label's counter by one returning device-scope atomic (memory-side, so
-// coherent across the XCDs' L2s), issued two tiles ahead in an epilogue (its latency hides under the epilogue's stores).
+// ranges, as xcd_remap does; the first item of every block is static (blockIdx / 8 within its label), every later one
+// is taken from its label's counter (only the label's blocks touch it) by one returning atomic, issued one tile ahead:
+// at the end of the previous epilogue (at kernel start for the second item), read back at the end of the main loop
+// (whose last waits are vmcnt(0)) and handed to every wave through LDS. One tile ahead keeps a label's in-flight items
+// within about one round of 32 consecutive tiles, the static walk's L2 footprint (two ahead spread them over two).
 // A block that starts late — its CU held by an RCCL kernel of a data-parallel wrapper, or by any concurrent kernel — so
 // takes fewer tiles instead of making the grid end on its last one. Taken (DYN) when the caller says collectives may
 // share the CUs (gpt2mi.h GPT2MI_SCHED_SHARED_CUS): alone on the GPU the static walk is 1-3 % faster (the grab's wait
@@ -341,12 +343,11 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   const int nsplit = PERSIST ? 1 : (P.K + P.k_per_split - 1) / P.k_per_split;
   int vid = blockIdx.x;  // PERSIST: virtual block id of this tile (blockIdx + i * gridDim, same XCD label)
   const int item = xcd_remap(vid, ntiles * nsplit);
-  // PERSIST, DYN: the block's XCD label range and the item of its NEXT tile (the second one static)
-  [[maybe_unused]] int q_base = 0, q_cnt = 0, nxt_item = -1;
+  // PERSIST, DYN: the block's XCD label range, the label's block count (its static items) and the item of its NEXT tile
+  [[maybe_unused]] int q_base = 0, q_cnt = 0, q_blocks = 0, nxt_item = -1;
   if constexpr (PERSIST && DYN) {
     xcd_range(blockIdx.x % 8, ntiles, q_base, q_cnt);
-    const int j1 = blockIdx.x / 8 + gridDim.x / 8;
-    nxt_item = j1 < q_cnt ? q_base + j1 : -1;
+    q_blocks = (gridDim.x + 7 - blockIdx.x % 8) / 8;
   }
   const int split = item / ntiles;
   int m0, n0;
@@ -420,6 +421,17 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   };
   char* buf0 = smem;
   char* buf1 = smem + kBuf;
+  // DYN: the queue counter's old value from this block's latest grab (thread 0; written by an asm atomic, so that no
+  // compiler-inserted vmcnt(0) drains the DMAs for its return; valid once a wait has retired it: read only at the end of
+  // the main loop, after its vmcnt(0) waits). The first grab (for the block's second tile) goes out before the prologue.
+  [[maybe_unused]] unsigned grab = 0u;
+  [[maybe_unused]] auto grab_next = [&]() {
+    if (threadIdx.x == 0) {
+      unsigned* qa = &g_pp_queue[P.qslot][blockIdx.x % 8];
+      asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(grab) : "v"(qa), "v"(1u) : "memory");
+    }
+  };
+  if constexpr (PERSIST && DYN) grab_next();
 
   // prologue: what phases -6..-1 would have issued (all of tile 0, A_0 / B_0 of tile 1), in order. The zero tile
   // of an odd count: the same DMAs with every lane's source redirected to 16 zero bytes (a select, no branch:
@@ -440,9 +452,6 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   PP_STAMP(1)
   if (wr == 1) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind group 0
   __builtin_amdgcn_sched_barrier(0);
-  // DYN: the queue counter's old value from this block's last grab (thread 0; written by an asm atomic, valid once a
-  // wait has retired it: read only at the end of the next main loop, after its vmcnt(0) waits)
-  [[maybe_unused]] unsigned grab = 0u;
   for (;;) {  // PERSIST: one iteration per output tile (non-persistent: exactly one)
 
   Frags fr;
@@ -523,15 +532,13 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   ktile(nkv - 2, I0{}, Tr{}, F{});
   ktile(nkv - 2, I1{}, F{}, F{});
   if constexpr (PERSIST && DYN) {
-    // the item of the tile after this one, from the grab of the last epilogue: the last K-tile's waits were vmcnt(0),
-    // so the atomic has returned (the empty asm keeps the read of `grab` below them)
-    if (after_epi) {
-      asm volatile("" : "+v"(grab));
-      if (threadIdx.x == 0) {
-        const int idx = (int)grab + 2 * (int)(gridDim.x / 8);
-        s_next = idx < q_cnt ? q_base + idx : -1;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      }
+    // the item of the tile after this one, from the latest grab: the last K-tile's waits were vmcnt(0), so the atomic
+    // has returned (the empty asm keeps the read of `grab` below them)
+    asm volatile("" : "+v"(grab));
+    if (threadIdx.x == 0) {
+      const int idx = (int)grab + q_blocks;
+      s_next = idx < q_cnt ? q_base + idx : -1;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
   }
   if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the groups (same barrier count)
@@ -539,7 +546,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   __builtin_amdgcn_sched_barrier(0);
   if constexpr (PERSIST && DYN) {
     asm volatile("" ::: "memory");
-    if (after_epi) nxt_item = __builtin_amdgcn_readfirstlane(s_next);
+    nxt_item = __builtin_amdgcn_readfirstlane(s_next);
   }
   PP_STAMP(2)
 
@@ -605,15 +612,6 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
       dma_b_at(next_n0, 0, 0, buf0);
       dma_b_at(next_n0, 0, 1, buf0);
       dma_a_at(next_m0, 0, 1, buf0);
-    }
-  }
-  // DYN: the tile after next from the label's counter (one lane; read back at the end of the next main loop). An asm
-  // atomic (relaxed, agent scope: sc0 returns the old value), so that no compiler-inserted vmcnt(0) drains this wave's
-  // DMAs and stores for its return (hipcc placed one right behind the builtin atomic: 1-3 % of the kernel)
-  if constexpr (PERSIST && DYN) {
-    if (has_next && threadIdx.x == 0) {
-      unsigned* qa = &g_pp_queue[P.qslot][blockIdx.x % 8];
-      asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(grab) : "v"(qa), "v"(1u) : "memory");
     }
   }
 
@@ -976,6 +974,9 @@ write_image(mi, wr * 64);
       }
       return;
     }
+    // DYN: the item of the tile after next (younger than this epilogue's stores, so the FIRST waits below never wait for
+    // it; the steady-state waits of the next main loop retire it behind 8 DMAs)
+    if constexpr (DYN) grab_next();
     // the next tile's prologue continues: A_0 / B_0 of its K-tile 1 into buffer 1 once every wave is done
     // with the image there, then the same counted wait as the first prologue (epilogue stores issued in
     // between only make it wait longer, never too little: outstanding <= 8 leaves >= 4 DMAs retired)

@@ -14,5 +14,3 @@ timeout -k 10 400 env LIB_AB_OP=gemm LIB_AB_IMPLS=0,1024 python tools/lib_ab.py 
   gpt_2_distributed_amd/libgpt2mi.so > $O/dyn_ab.log 2>&1 || exit $?
 tail -12 $O/dyn_ab.log
 TAG=$T bash tools/gpu_r4_bench.sh || exit $?
-timeout -k 10 300 python tools/hipblaslt_probe.py > $O/hipblaslt.log 2>&1 || exit $?
-cat $O/hipblaslt.log
