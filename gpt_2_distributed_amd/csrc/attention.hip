@@ -46,6 +46,13 @@ GPT2MI_PRODUCT_KNOB(ATTN_FWD_OCC, 3);
 GPT2MI_PRODUCT_KNOB(ATTN_FWD_LMAX, 1);
 GPT2MI_PRODUCT_KNOB(ATTN_DKDV_SB, 1);
 GPT2MI_PRODUCT_KNOB(ATTN_DKDV_WAVES, 4);
+// dK/dV tile order: 0 = per 32-query half S/dP -> elementwise -> dV/dK; 1 = the second half's S/dP MFMAs issued before
+// the first half's dV/dK, so the second half's elementwise (VALU) runs beside the first half's dV/dK (MFMA);
+// 2 = as 1 with the compiler told to interleave them (sched_group_barrier)
+#ifndef ATTN_DKDV_PIPE
+#define ATTN_DKDV_PIPE 0
+#endif
+GPT2MI_PRODUCT_KNOB(ATTN_DKDV_PIPE, 0);
 constexpr int kDkdvWaves = ATTN_DKDV_WAVES;  // waves per dK/dV workgroup (32 keys each)
 constexpr int BKB = 32 * kDkdvWaves;        // keys per workgroup in dK/dV
 constexpr int BQT = 64;  // queries per Q/dO tile in dK/dV
@@ -588,6 +595,101 @@ __global__ __launch_bounds__(64 * kDkdvWaves) __attribute__((amdgpu_waves_per_eu
     if (wave_valid && q0 + BQT - 1 >= k_lo) {  // wave-uniform: a query of the tile sees a key of the wave
       const bool diag = q0 < k_lo + 31;
       const uint32_t pre_t = DROP ? drop_pre(seed32(seed), ((uint32_t)bh * T + q0 + 4 * g) * (uint32_t)T + k_lo + (lane & 15)) : 0u;
+#if ATTN_DKDV_PIPE
+      // S / dP of 32-query half hq: s, dp [kg][fl] = S[q = q0 + 16(2hq+fl) + 4g + r][key = k_lo + 16kg + (l&15)]
+      auto sdp = [&](int hq, f32x4 (&s)[2][2], f32x4 (&dp)[2][2], f32x4 (&l4)[2], f32x4 (&d4)[2]) {
+#pragma unroll
+        for (int fl = 0; fl < 2; ++fl) {
+          l4[fl] = *reinterpret_cast<const f32x4*>(Ls + 16 * (2 * hq + fl) + 4 * g);
+          d4[fl] = *reinterpret_cast<const f32x4*>(Dl + 16 * (2 * hq + fl) + 4 * g);
+        }
+#pragma unroll
+        for (int fl = 0; fl < 2; ++fl) {
+          const int fi = 2 * hq + fl;
+          s[0][fl] = s[1][fl] = f32x4{0.f, 0.f, 0.f, 0.f};
+          dp[0][fl] = dp[1][fl] = -d4[fl];
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) {
+            const bf16x8 qa = row_frag(Qs, 16 * fi, kk, lane);
+            const bf16x8 da = row_frag(Ds, 16 * fi, kk, lane);
+#pragma unroll
+            for (int kg = 0; kg < 2; ++kg) {
+              s[kg][fl] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[kg][kk], s[kg][fl], 0, 0, 0);
+              dp[kg][fl] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, vf[kg][kk], dp[kg][fl], 0, 0, 0);
+            }
+          }
+        }
+      };
+      // P, dS of half hq, packed: pk = {P_drop kg 0, P_drop kg 1, dS kg 0, dS kg 1}
+      auto elem = [&](auto diag_c, int hq, f32x4 (&s)[2][2], f32x4 (&dp)[2][2], const f32x4 (&l4)[2],
+                      const f32x4 (&d4)[2], bf16x8 (&pk)[4]) {
+        constexpr bool DIAG = decltype(diag_c)::value;
+#pragma unroll
+        for (int kg = 0; kg < 2; ++kg) {
+          const int key = k_lo + 16 * kg + (lane & 15);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            uint32_t km[2] = {~0u, ~0u};
+            if constexpr (DROP)
+              drop_keep_masks(tk2, drop_fin(pre_t + ((uint32_t)(32 * hq + r) * (uint32_t)T + 16u * kg) * kDropC1,
+                                            seed_kx(seed)), km[0], km[1]);
+#pragma unroll
+            for (int fl = 0; fl < 2; ++fl) {
+              float p = __builtin_amdgcn_exp2f(fmaf(s[kg][fl][r], sl2, -l4[fl][r]));
+              if constexpr (DIAG) p = (q0 + 16 * (2 * hq + fl) + 4 * g + r < key) ? 0.f : p;
+              float pdv = p, d = dp[kg][fl][r];
+              if constexpr (DROP) {
+                pdv = __uint_as_float(km[fl] & __float_as_uint(p));
+                d = sel_mask(km[fl], d, -d4[fl][r]);
+              }
+              dp[kg][fl][r] = pdv;
+              s[kg][fl][r] = p * d;
+            }
+          }
+        }
+        pk[0] = pack_perm(dp[0], 0);
+        pk[1] = pack_perm(dp[1], 0);
+        pk[2] = pack_perm(s[0], 0);
+        pk[3] = pack_perm(s[1], 0);
+      };
+      auto dvdk = [&](int hq, const bf16x8 (&pk)[4]) {
+#pragma unroll
+        for (int fd = 0; fd < 4; ++fd) {
+          const bf16x8 dot = tr_frag(Ds, hq, 16 * fd, lane);
+          const bf16x8 qt = tr_frag(Qs, hq, 16 * fd, lane);
+          dv[0][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dot, pk[0], dv[0][fd], 0, 0, 0);
+          dv[1][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dot, pk[1], dv[1][fd], 0, 0, 0);
+          dk[0][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qt, pk[2], dk[0][fd], 0, 0, 0);
+          dk[1][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qt, pk[3], dk[1][fd], 0, 0, 0);
+        }
+      };
+      // half 0: S/dP, elementwise; half 1's S/dP issued next, then half 0's dV/dK beside half 1's elementwise
+      auto tile = [&](auto diag_c) {
+        f32x4 sa[2][2], dpa[2][2], la[2], da[2], sb[2][2], dpb[2][2], lb[2], db[2];
+        bf16x8 pa[4], pb[4];
+        sdp(0, sa, dpa, la, da);
+        elem(diag_c, 0, sa, dpa, la, da, pa);
+        sdp(1, sb, dpb, lb, db);
+        __builtin_amdgcn_sched_barrier(0);
+        dvdk(0, pa);
+        elem(diag_c, 1, sb, dpb, lb, db, pb);
+#if ATTN_DKDV_PIPE == 2
+        // 16 MFMAs of half 0's dV/dK, each followed by a share of half 1's elementwise VALU (and the fragment reads)
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+          __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);  // 6 VALU
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+        }
+#endif
+        __builtin_amdgcn_sched_barrier(0);
+        dvdk(1, pb);
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      if (diag) tile(std::true_type{});
+      else tile(std::false_type{});
+    }
+#else
       // Two 32-query halves per 64-query tile; each half is exactly one MFMA k-step of the dV/dK
       // products, so only half of S / dP is live at a time (register pressure -> occupancy).
 #pragma unroll
@@ -663,6 +765,7 @@ __global__ __launch_bounds__(64 * kDkdvWaves) __attribute__((amdgpu_waves_per_eu
 #endif
       }
     }
+#endif
     if (i + 1 < nqt) sstore(smem + (cur ^ 1) * kStage);
     __syncthreads();
   }
