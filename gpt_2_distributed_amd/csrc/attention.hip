@@ -53,6 +53,12 @@ GPT2MI_PRODUCT_KNOB(ATTN_DKDV_WAVES, 4);
 #define ATTN_DKDV_PIPE 0
 #endif
 GPT2MI_PRODUCT_KNOB(ATTN_DKDV_PIPE, 0);
+// dQ tile order: 0 = S/dP of the 64-key tile -> elementwise -> dQ; 1 = per 32-key half, the second half's S/dP issued
+// before the first half's dQ MFMAs, which then run beside the second half's elementwise
+#ifndef ATTN_DQ_PIPE
+#define ATTN_DQ_PIPE 0
+#endif
+GPT2MI_PRODUCT_KNOB(ATTN_DQ_PIPE, 0);
 constexpr int kDkdvWaves = ATTN_DKDV_WAVES;  // waves per dK/dV workgroup (32 keys each)
 constexpr int BKB = 32 * kDkdvWaves;        // keys per workgroup in dK/dV
 constexpr int BQT = 64;  // queries per Q/dO tile in dK/dV
@@ -444,6 +450,80 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const bf16* __
       tile_dma(nxt + BKV * 128, rs, (j + 1) * BKV, 2 * C + h * D, (int)ld, loff, wu);
     }
     const int k_lo = j * BKV;
+#if ATTN_DQ_PIPE
+    if (wave_valid && k_lo <= q_lo + 31) {
+      const bool diag = k_lo + BKV - 1 > q_lo;
+      [[maybe_unused]] uint32_t pre = 0;
+      if constexpr (DROP)
+        pre = drop_pre(seed32(seed), ((uint32_t)bh * T + q_lo + (lane & 15)) * (uint32_t)T + k_lo + 4 * g);
+      // S / dP of the 32 keys of half kk (fi = 2kk + f): s, dp [qg][f]
+      auto sdp = [&](int kk, f32x4 (&s)[2][2], f32x4 (&dp)[2][2]) {
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+          const int fi = 2 * kk + f;
+          s[0][f] = s[1][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+          dp[0][f] = f32x4{-dl[0], -dl[0], -dl[0], -dl[0]};
+          dp[1][f] = f32x4{-dl[1], -dl[1], -dl[1], -dl[1]};
+#pragma unroll
+          for (int k2 = 0; k2 < 2; ++k2) {
+            const bf16x8 kf = row_frag(Ks, 16 * fi, k2, lane);
+            const bf16x8 vf = row_frag(Vs, 16 * fi, k2, lane);
+#pragma unroll
+            for (int qg = 0; qg < 2; ++qg) {
+              s[qg][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qg][k2], s[qg][f], 0, 0, 0);
+              dp[qg][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, df[qg][k2], dp[qg][f], 0, 0, 0);
+            }
+          }
+        }
+      };
+      // dS of half kk, packed per query group
+      auto elem = [&](auto diag_c, int kk, f32x4 (&s)[2][2], const f32x4 (&dp)[2][2], bf16x8 (&pk)[2]) {
+        constexpr bool DIAG = decltype(diag_c)::value;
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+          const int fi = 2 * kk + f;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            uint32_t km[2] = {~0u, ~0u};
+            if constexpr (DROP)
+              drop_keep_masks(tk2, drop_fin(pre + (uint32_t)(16 * fi + r) * kDropC1, seed_kx(seed)), km[0], km[1]);
+#pragma unroll
+            for (int qg = 0; qg < 2; ++qg) {
+              float p = __builtin_amdgcn_exp2f(fmaf(s[qg][f][r], sl2, -lse2[qg]));
+              if constexpr (DIAG) p = (k_lo + 16 * fi + 4 * g + r > q_lo + 16 * qg + (lane & 15)) ? 0.f : p;
+              float d = dp[qg][f][r];
+              if constexpr (DROP) d = sel_mask(km[qg], d, -dl[qg]);
+              s[qg][f][r] = p * d;
+            }
+          }
+        }
+        pk[0] = pack_perm(s[0], 0);
+        pk[1] = pack_perm(s[1], 0);
+      };
+      auto dqm = [&](int kk, const bf16x8 (&pk)[2]) {
+#pragma unroll
+        for (int fd = 0; fd < 4; ++fd) {
+          const bf16x8 kt = tr_frag(Ks, kk, 16 * fd, lane);
+          dq[0][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kt, pk[0], dq[0][fd], 0, 0, 0);
+          dq[1][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kt, pk[1], dq[1][fd], 0, 0, 0);
+        }
+      };
+      auto tile = [&](auto diag_c) {
+        f32x4 sa[2][2], dpa[2][2], sb[2][2], dpb[2][2];
+        bf16x8 pa[2], pb[2];
+        sdp(0, sa, dpa);
+        elem(diag_c, 0, sa, dpa, pa);
+        sdp(1, sb, dpb);
+        __builtin_amdgcn_sched_barrier(0);
+        dqm(0, pa);
+        elem(diag_c, 1, sb, dpb, pb);
+        __builtin_amdgcn_sched_barrier(0);
+        dqm(1, pb);
+      };
+      if (diag) tile(std::true_type{});
+      else tile(std::false_type{});
+    }
+#else
     if (wave_valid && k_lo <= q_lo + 31) {
       const bool diag = k_lo + BKV - 1 > q_lo;
       f32x4 s[2][4], dp[2][4];
@@ -500,6 +580,7 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const bf16* __
         }
       }
     }
+#endif
     __syncthreads();
   }
   if (!wave_valid) return;
