@@ -36,29 +36,12 @@ constexpr int BKV = 64;  // keys per K/V tile in fwd / dQ
 #ifndef ATTN_FWD_LMAX
 #define ATTN_FWD_LMAX 1  // forward rescale test on each lane's own scores (0: cross-lane max every tile, A/B builds)
 #endif
-#ifndef ATTN_DKDV_SB
-#define ATTN_DKDV_SB 1  // dK/dV: scheduling barrier between the two 32-query halves of a tile (0: A/B builds)
-#endif
 #ifndef ATTN_DKDV_WAVES
 #define ATTN_DKDV_WAVES 4
 #endif
 GPT2MI_PRODUCT_KNOB(ATTN_FWD_OCC, 3);
 GPT2MI_PRODUCT_KNOB(ATTN_FWD_LMAX, 1);
-GPT2MI_PRODUCT_KNOB(ATTN_DKDV_SB, 1);
 GPT2MI_PRODUCT_KNOB(ATTN_DKDV_WAVES, 4);
-// dK/dV tile order: 0 = per 32-query half S/dP -> elementwise -> dV/dK; 1 = the second half's S/dP MFMAs issued before
-// the first half's dV/dK, so the second half's elementwise (VALU) runs beside the first half's dV/dK (MFMA);
-// 2 = as 1 with the compiler told to interleave them (sched_group_barrier)
-#ifndef ATTN_DKDV_PIPE
-#define ATTN_DKDV_PIPE 0
-#endif
-GPT2MI_PRODUCT_KNOB(ATTN_DKDV_PIPE, 0);
-// dQ tile order: 0 = S/dP of the 64-key tile -> elementwise -> dQ; 1 = per 32-key half, the second half's S/dP issued
-// before the first half's dQ MFMAs, which then run beside the second half's elementwise
-#ifndef ATTN_DQ_PIPE
-#define ATTN_DQ_PIPE 0
-#endif
-GPT2MI_PRODUCT_KNOB(ATTN_DQ_PIPE, 0);
 constexpr int kDkdvWaves = ATTN_DKDV_WAVES;  // waves per dK/dV workgroup (32 keys each)
 constexpr int BKB = 32 * kDkdvWaves;        // keys per workgroup in dK/dV
 constexpr int BQT = 64;  // queries per Q/dO tile in dK/dV
@@ -380,9 +363,12 @@ __global__ __launch_bounds__(kThreads, ATTN_FWD_OCC) void attn_fwd_kernel(const 
 // ---------------------------------------------------------------------------------------------
 // dQ: query-outer; recomputes P from the saved LSE. dS^T = P^T o (dP^T - delta), dQ^T += K^T dS^T.
 // delta = rowsum(dO o O) of the wave's own queries is formed here (no separate pass) and written out for
-// the dK/dV kernel, which runs after this one.
+// the dK/dV kernel, which runs after this one. A 64-key tile runs as two 32-key halves, the second half's S / dP MFMAs
+// issued ahead of the first half's dQ MFMAs so that those run beside the second half's elementwise VALU work (a
+// software pipeline inside one wave; the half-size S / dP registers also bring the kernel to 160 VGPRs: 3 waves / SIMD;
+// backward 575.5 -> 555.6 us, profiles/r4l/attn.log).
 template <bool DROP>
-__global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const bf16* __restrict__ qkv,
+__global__ __launch_bounds__(kThreads, 3) void attn_bwd_dq_kernel(const bf16* __restrict__ qkv,
                                                                   const bf16* __restrict__ out,
                                                                   const bf16* __restrict__ dout,
                                                                   const float* __restrict__ lse,
@@ -450,7 +436,6 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const bf16* __
       tile_dma(nxt + BKV * 128, rs, (j + 1) * BKV, 2 * C + h * D, (int)ld, loff, wu);
     }
     const int k_lo = j * BKV;
-#if ATTN_DQ_PIPE
     if (wave_valid && k_lo <= q_lo + 31) {
       const bool diag = k_lo + BKV - 1 > q_lo;
       [[maybe_unused]] uint32_t pre = 0;
@@ -523,64 +508,6 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const bf16* __
       if (diag) tile(std::true_type{});
       else tile(std::false_type{});
     }
-#else
-    if (wave_valid && k_lo <= q_lo + 31) {
-      const bool diag = k_lo + BKV - 1 > q_lo;
-      f32x4 s[2][4], dp[2][4];
-#pragma unroll
-      for (int fi = 0; fi < 4; ++fi) {
-        // dP' accumulates onto -delta (the query's row constant), so a kept entry's dP' - delta leaves the chain
-        s[0][fi] = s[1][fi] = f32x4{0.f, 0.f, 0.f, 0.f};
-        dp[0][fi] = f32x4{-dl[0], -dl[0], -dl[0], -dl[0]};
-        dp[1][fi] = f32x4{-dl[1], -dl[1], -dl[1], -dl[1]};
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-          const bf16x8 kf = row_frag(Ks, 16 * fi, kk, lane);
-          const bf16x8 vf = row_frag(Vs, 16 * fi, kk, lane);
-#pragma unroll
-          for (int qg = 0; qg < 2; ++qg) {
-            s[qg][fi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qg][kk], s[qg][fi], 0, 0, 0);
-            dp[qg][fi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, df[qg][kk], dp[qg][fi], 0, 0, 0);
-          }
-        }
-      }
-      // dS^T = P^T o (dP'^T - delta): dropped entries get dP = 0 (same (q, q^16)-pair hash as the forward)
-      auto elementwise = [&](auto diag_c) {
-        constexpr bool DIAG = decltype(diag_c)::value;
-        uint32_t pre = 0;
-        if constexpr (DROP)
-          pre = drop_pre(seed32(seed), ((uint32_t)bh * T + q_lo + (lane & 15)) * (uint32_t)T + k_lo + 4 * g);
-#pragma unroll
-        for (int fi = 0; fi < 4; ++fi)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            uint32_t km[2] = {~0u, ~0u};  // keep masks of queries q (qg 0) and q ^ 16 (qg 1): one hash
-            if constexpr (DROP)
-              drop_keep_masks(tk2, drop_fin(pre + (uint32_t)(16 * fi + r) * kDropC1, seed_kx(seed)), km[0], km[1]);
-#pragma unroll
-            for (int qg = 0; qg < 2; ++qg) {
-              float p = __builtin_amdgcn_exp2f(fmaf(s[qg][fi][r], sl2, -lse2[qg]));
-              if constexpr (DIAG) p = (k_lo + 16 * fi + 4 * g + r > q_lo + 16 * qg + (lane & 15)) ? 0.f : p;
-              float d = dp[qg][fi][r];  // dP' - delta
-              if constexpr (DROP) d = sel_mask(km[qg], d, -dl[qg]);
-              s[qg][fi][r] = p * d;
-            }
-          }
-      };
-      if (diag) elementwise(std::true_type{});
-      else elementwise(std::false_type{});
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const bf16x8 s0 = pack_perm(s[0], kk), s1 = pack_perm(s[1], kk);
-#pragma unroll
-        for (int fd = 0; fd < 4; ++fd) {
-          const bf16x8 kt = tr_frag(Ks, kk, 16 * fd, lane);
-          dq[0][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kt, s0, dq[0][fd], 0, 0, 0);
-          dq[1][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kt, s1, dq[1][fd], 0, 0, 0);
-        }
-      }
-    }
-#endif
     __syncthreads();
   }
   if (!wave_valid) return;
@@ -597,7 +524,9 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_dq_kernel(const bf16* __
 }
 
 // ---------------------------------------------------------------------------------------------
-// dK, dV: key-outer (128 keys per workgroup, 32 per wave) over 64-query tiles at or after the keys.
+// dK, dV: key-outer (128 keys per workgroup, 32 per wave) over 64-query tiles at or after the keys. Each tile runs as
+// two 32-query halves, the second half's S / dP MFMAs issued ahead of the first half's dV / dK MFMAs, which then run
+// beside the second half's elementwise work (with the dQ change: backward 575.5 -> 547.0 us, profiles/r4l/attn.log).
 template <bool DROP>
 __global__ __launch_bounds__(64 * kDkdvWaves) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_bwd_dkdv_kernel(const bf16* __restrict__ qkv,
                                                                     const bf16* __restrict__ dout,
@@ -676,7 +605,6 @@ __global__ __launch_bounds__(64 * kDkdvWaves) __attribute__((amdgpu_waves_per_eu
     if (wave_valid && q0 + BQT - 1 >= k_lo) {  // wave-uniform: a query of the tile sees a key of the wave
       const bool diag = q0 < k_lo + 31;
       const uint32_t pre_t = DROP ? drop_pre(seed32(seed), ((uint32_t)bh * T + q0 + 4 * g) * (uint32_t)T + k_lo + (lane & 15)) : 0u;
-#if ATTN_DKDV_PIPE
       // S / dP of 32-query half hq: s, dp [kg][fl] = S[q = q0 + 16(2hq+fl) + 4g + r][key = k_lo + 16kg + (l&15)]
       auto sdp = [&](int hq, f32x4 (&s)[2][2], f32x4 (&dp)[2][2], f32x4 (&l4)[2], f32x4 (&d4)[2]) {
 #pragma unroll
@@ -754,15 +682,6 @@ __global__ __launch_bounds__(64 * kDkdvWaves) __attribute__((amdgpu_waves_per_eu
         __builtin_amdgcn_sched_barrier(0);
         dvdk(0, pa);
         elem(diag_c, 1, sb, dpb, lb, db, pb);
-#if ATTN_DKDV_PIPE == 2
-        // 16 MFMAs of half 0's dV/dK, each followed by a share of half 1's elementwise VALU (and the fragment reads)
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
-          __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);  // 6 VALU
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
-        }
-#endif
         __builtin_amdgcn_sched_barrier(0);
         dvdk(1, pb);
         __builtin_amdgcn_sched_barrier(0);
@@ -770,83 +689,6 @@ __global__ __launch_bounds__(64 * kDkdvWaves) __attribute__((amdgpu_waves_per_eu
       if (diag) tile(std::true_type{});
       else tile(std::false_type{});
     }
-#else
-      // Two 32-query halves per 64-query tile; each half is exactly one MFMA k-step of the dV/dK
-      // products, so only half of S / dP is live at a time (register pressure -> occupancy).
-#pragma unroll
-      for (int hq = 0; hq < 2; ++hq) {
-        f32x4 s[2][2], dp[2][2];  // [kg][fl]: S[q = q0 + 16(2hq+fl) + 4g + r][key = k_lo + 16kg + (l&15)]
-        f32x4 l4[2], d4[2];
-#pragma unroll
-        for (int fl = 0; fl < 2; ++fl) {
-          l4[fl] = *reinterpret_cast<const f32x4*>(Ls + 16 * (2 * hq + fl) + 4 * g);
-          d4[fl] = *reinterpret_cast<const f32x4*>(Dl + 16 * (2 * hq + fl) + 4 * g);
-        }
-#pragma unroll
-        for (int fl = 0; fl < 2; ++fl) {
-          const int fi = 2 * hq + fl;
-          // dP' accumulates onto -delta (the rows' constants), so a kept entry's dP' - delta leaves the chain
-          s[0][fl] = s[1][fl] = f32x4{0.f, 0.f, 0.f, 0.f};
-          dp[0][fl] = dp[1][fl] = -d4[fl];
-#pragma unroll
-          for (int kk = 0; kk < 2; ++kk) {
-            const bf16x8 qa = row_frag(Qs, 16 * fi, kk, lane);
-            const bf16x8 da = row_frag(Ds, 16 * fi, kk, lane);
-#pragma unroll
-            for (int kg = 0; kg < 2; ++kg) {
-              s[kg][fl] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[kg][kk], s[kg][fl], 0, 0, 0);
-              dp[kg][fl] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, vf[kg][kk], dp[kg][fl], 0, 0, 0);
-            }
-          }
-        }
-        // P = exp2(S*scale*log2e - LSE*log2e); dropped entries: P_drop = 0 (dV; its 1/(1-p) is applied
-        // to dV at the end) and dP = 0 (dS); dP already carries 1/(1-p) through the prescaled V.
-        auto elementwise = [&](auto diag_c) {
-          constexpr bool DIAG = decltype(diag_c)::value;
-#pragma unroll
-          for (int kg = 0; kg < 2; ++kg) {
-            const int key = k_lo + 16 * kg + (lane & 15);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              uint32_t km[2] = {~0u, ~0u};  // queries q and q^16 (fl = 0, 1) share one dropout hash
-              // counter (bh*T + q0 + 4g + 32hq + r) * T + key: a lane base plus (32hq + r) * T + 16kg (uniform)
-              if constexpr (DROP)
-                drop_keep_masks(tk2, drop_fin(pre_t + ((uint32_t)(32 * hq + r) * (uint32_t)T + 16u * kg) * kDropC1,
-                                              seed_kx(seed)), km[0], km[1]);
-#pragma unroll
-              for (int fl = 0; fl < 2; ++fl) {
-                float p = __builtin_amdgcn_exp2f(fmaf(s[kg][fl][r], sl2, -l4[fl][r]));
-                if constexpr (DIAG) p = (q0 + 16 * (2 * hq + fl) + 4 * g + r < key) ? 0.f : p;
-                float pdv = p, d = dp[kg][fl][r];  // dP' - delta
-                if constexpr (DROP) {
-                  pdv = __uint_as_float(km[fl] & __float_as_uint(p));
-                  d = sel_mask(km[fl], d, -d4[fl][r]);
-                }
-                dp[kg][fl][r] = pdv;  // dropped P (for dV)
-                s[kg][fl][r] = p * d;  // dS
-              }
-            }
-          }
-        };
-        if (diag) elementwise(std::true_type{});
-        else elementwise(std::false_type{});
-        const bf16x8 p0 = pack_perm(dp[0], 0), p1 = pack_perm(dp[1], 0);
-        const bf16x8 s0 = pack_perm(s[0], 0), s1 = pack_perm(s[1], 0);
-#pragma unroll
-        for (int fd = 0; fd < 4; ++fd) {
-          const bf16x8 dot = tr_frag(Ds, hq, 16 * fd, lane);
-          const bf16x8 qt = tr_frag(Qs, hq, 16 * fd, lane);
-          dv[0][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dot, p0, dv[0][fd], 0, 0, 0);
-          dv[1][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dot, p1, dv[1][fd], 0, 0, 0);
-          dk[0][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qt, s0, dk[0][fd], 0, 0, 0);
-          dk[1][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qt, s1, dk[1][fd], 0, 0, 0);
-        }
-#if ATTN_DKDV_SB
-        __builtin_amdgcn_sched_barrier(0);
-#endif
-      }
-    }
-#endif
     if (i + 1 < nqt) sstore(smem + (cur ^ 1) * kStage);
     __syncthreads();
   }
