@@ -42,12 +42,6 @@ constexpr int BKV = 64;  // keys per K/V tile in fwd / dQ
 GPT2MI_PRODUCT_KNOB(ATTN_FWD_OCC, 3);
 GPT2MI_PRODUCT_KNOB(ATTN_FWD_LMAX, 1);
 GPT2MI_PRODUCT_KNOB(ATTN_DKDV_WAVES, 4);
-// forward tile order: 0 = S of the 64-key tile -> softmax -> P.V; 1 = two 32-key halves, the second half's S MFMAs
-// issued ahead of the first half's P.V (its softmax runs beside them; rescale decisions per half)
-#ifndef ATTN_FWD_PIPE
-#define ATTN_FWD_PIPE 0
-#endif
-GPT2MI_PRODUCT_KNOB(ATTN_FWD_PIPE, 0);
 constexpr int kDkdvWaves = ATTN_DKDV_WAVES;  // waves per dK/dV workgroup (32 keys each)
 constexpr int BKB = 32 * kDkdvWaves;        // keys per workgroup in dK/dV
 constexpr int BQT = 64;  // queries per Q/dO tile in dK/dV
@@ -93,10 +87,7 @@ __device__ __forceinline__ float xor_sum(float v) {
 }
 // max of a lane's 16 scores as a v_max3 tree: 8 instructions (5 + 2 + 1)
 __device__ __forceinline__ float max3f(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
-// max of a lane's 8 scores (a 32-key half)
-__device__ __forceinline__ float max8(const f32x4 (&s)[2]) {
-  return fmaxf(max3f(s[0][0], s[0][1], s[0][2]), max3f(max3f(s[0][3], s[1][0], s[1][1]), s[1][2], s[1][3]));
-}
+
 __device__ __forceinline__ float max16(const f32x4 (&s)[4]) {
   const float t0 = max3f(s[0][0], s[0][1], s[0][2]), t1 = max3f(s[0][3], s[1][0], s[1][1]);
   const float t2 = max3f(s[1][2], s[1][3], s[2][0]), t3 = max3f(s[2][1], s[2][2], s[2][3]);
@@ -255,108 +246,6 @@ __global__ __launch_bounds__(kThreads, ATTN_FWD_OCC) void attn_fwd_kernel(const 
     const int k_lo = j * BKV;
     // wave-uniform: a key of the tile is visible to a query of the wave
     const bool active = wave_valid && k_lo <= q_lo + 31;
-#if ATTN_FWD_PIPE
-    // S of 32-key half hh: s[qg][f] = keys k_lo + 16(2hh + f) + 4g + r of query q_lo + 16qg + (l & 15)
-    auto shalf = [&](int hh, f32x4 (&sc)[2][2]) {
-#pragma unroll
-      for (int f = 0; f < 2; ++f) {
-        const int fi = 2 * hh + f;
-        sc[0][f] = sc[1][f] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-          const bf16x8 kf = row_frag(Ks, 16 * fi, kk, lane);
-          sc[0][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[0][kk], sc[0][f], 0, 0, 0);
-          sc[1][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[1][kk], sc[1][f], 0, 0, 0);
-        }
-      }
-    };
-    [[maybe_unused]] uint32_t pre = 0, tk2 = 0;
-    if constexpr (DROP) {
-      pre = drop_pre(seed32(seed), ((uint32_t)bh * T + q_lo + (lane & 15)) * (uint32_t)T + k_lo + 4 * g);
-      tk2 = drop_tk2(thr);
-    }
-    // softmax of half hh (causal mask on a diagonal tile, the defer-max rescale decided on the half, exp), then P
-    // packed and dropped: pk[qg]
-    auto soft = [&](int hh, bool diag, f32x4 (&sc)[2][2], bf16x8 (&pk)[2], bf16x8 (&pu)[2]) {
-      if (diag) {
-#pragma unroll
-        for (int qg = 0; qg < 2; ++qg)
-#pragma unroll
-          for (int f = 0; f < 2; ++f)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              if (k_lo + 16 * (2 * hh + f) + 4 * g + r > q_lo + 16 * qg + (lane & 15)) sc[qg][f][r] = -INFINITY;
-      }
-#pragma unroll
-      for (int qg = 0; qg < 2; ++qg) {
-        const float lmax = max8(sc[qg]);
-        if (!__all(lmax * sl2 <= m[qg] + kRescaleThr)) {
-          const float cand = xor_max(lmax) * sl2;
-          const float mn = fmaxf(m[qg], cand);  // finite: the first half of tile 0 holds key 0, visible to every query
-          const float corr = __builtin_amdgcn_exp2f(m[qg] - mn);
-#pragma unroll
-          for (int f = 0; f < 4; ++f)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) o[qg][f][r] *= corr;
-          o[qg][4][0] *= corr;
-          m[qg] = mn;
-        }
-#pragma unroll
-        for (int f = 0; f < 2; ++f)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) sc[qg][f][r] = __builtin_amdgcn_exp2f(fmaf(sc[qg][f][r], sl2, -m[qg]));
-      }
-      pu[0] = pack_perm(sc[0], 0);
-      pu[1] = pack_perm(sc[1], 0);
-      pk[0] = pu[0];
-      pk[1] = pu[1];
-      if constexpr (DROP) {
-        u32x4 w0 = __builtin_bit_cast(u32x4, pk[0]), w1 = __builtin_bit_cast(u32x4, pk[1]);
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {
-          const uint32_t c = 16 * (2 * hh + (d >> 1)) + 2 * (d & 1);
-          const uint32_t ka = drop_keep_mask2(tk2, drop_fin(pre + c * kDropC1, seed_kx(seed)));
-          const uint32_t kb = drop_keep_mask2(tk2, drop_fin(pre + (c + 1) * kDropC1, seed_kx(seed)));
-          w0[d] &= __builtin_amdgcn_perm(kb, ka, 0x0A0A0808u);
-          w1[d] &= __builtin_amdgcn_perm(kb, ka, 0x0B0B0909u);
-        }
-        pk[0] = __builtin_bit_cast(bf16x8, w0);
-        pk[1] = __builtin_bit_cast(bf16x8, w1);
-      }
-    };
-    // row sums (undropped P) and P.V of half hh
-    auto pv = [&](int hh, const bf16x8 (&pk)[2], const bf16x8 (&pu)[2]) {
-      o[0][4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pu[0], o[0][4], 0, 0, 0);
-      o[1][4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pu[1], o[1][4], 0, 0, 0);
-#pragma unroll
-      for (int fd = 0; fd < 4; ++fd) {
-        const bf16x8 vt = tr_frag(Vs, hh, 16 * fd, lane);
-        o[0][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vt, pk[0], o[0][fd], 0, 0, 0);
-        o[1][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vt, pk[1], o[1][fd], 0, 0, 0);
-      }
-    };
-    f32x4 sa[2][2], sb[2][2];
-    bf16x8 pa[2], ua[2], pb[2], ub[2];
-    if (active) shalf(0, sa);
-    // next K/V tile straight into the other LDS stage (read last in tile j-1, released by its barrier)
-    if (j + 1 < nkv) {
-      char* nxt = smem + (cur ^ 1) * 2 * BKV * 128;
-      tile_dma(nxt, rs, (j + 1) * BKV, C + h * D, (int)ld, loff, wu);
-      tile_dma(nxt + BKV * 128, rs, (j + 1) * BKV, 2 * C + h * D, (int)ld, loff, wu);
-    }
-    if (active) {
-      const bool diag = k_lo + BKV - 1 > q_lo;
-      soft(0, diag, sa, pa, ua);
-      // a second half with every key past the wave's queries (diagonal tile, first 16-query group of the wave ... the
-      // whole half masked) still runs: its P is 0 after the mask, as in the one-pass tile
-      shalf(1, sb);
-      __builtin_amdgcn_sched_barrier(0);
-      pv(0, pa, ua);
-      soft(1, diag, sb, pb, ub);
-      __builtin_amdgcn_sched_barrier(0);
-      pv(1, pb, ub);
-    }
-#else
     f32x4 s[2][4];
     if (active) {
 #pragma unroll
@@ -458,7 +347,6 @@ __global__ __launch_bounds__(kThreads, ATTN_FWD_OCC) void attn_fwd_kernel(const 
         }
       }
     }
-#endif
     __syncthreads();
   }
   if (!wave_valid) return;
@@ -478,8 +366,7 @@ __global__ __launch_bounds__(kThreads, ATTN_FWD_OCC) void attn_fwd_kernel(const 
 // delta = rowsum(dO o O) of the wave's own queries is formed here (no separate pass) and written out for
 // the dK/dV kernel, which runs after this one. A 64-key tile runs as two 32-key halves, the second half's S / dP MFMAs
 // issued ahead of the first half's dQ MFMAs so that those run beside the second half's elementwise VALU work (a
-// software pipeline inside one wave; the half-size S / dP registers also bring the kernel to 160 VGPRs: 3 waves / SIMD;
-// backward 575.5 -> 555.6 us, profiles/r4l/attn.log).
+// software pipeline inside one wave; the half-size S / dP registers also bring the kernel to 160 VGPRs: 3 waves / SIMD).
 template <bool DROP>
 __global__ __launch_bounds__(kThreads, 3) void attn_bwd_dq_kernel(const bf16* __restrict__ qkv,
                                                                   const bf16* __restrict__ out,
@@ -639,7 +526,7 @@ __global__ __launch_bounds__(kThreads, 3) void attn_bwd_dq_kernel(const bf16* __
 // ---------------------------------------------------------------------------------------------
 // dK, dV: key-outer (128 keys per workgroup, 32 per wave) over 64-query tiles at or after the keys. Each tile runs as
 // two 32-query halves, the second half's S / dP MFMAs issued ahead of the first half's dV / dK MFMAs, which then run
-// beside the second half's elementwise work (with the dQ change: backward 575.5 -> 547.0 us, profiles/r4l/attn.log).
+// beside the second half's elementwise work (with the dQ change: backward 584.3 -> 577.9 us, profiles/r4n/attn_ab.log).
 template <bool DROP>
 __global__ __launch_bounds__(64 * kDkdvWaves) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_bwd_dkdv_kernel(const bf16* __restrict__ qkv,
                                                                     const bf16* __restrict__ dout,
