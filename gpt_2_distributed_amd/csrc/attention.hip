@@ -524,9 +524,8 @@ __global__ __launch_bounds__(kThreads, 3) void attn_bwd_dq_kernel(const bf16* __
 }
 
 // ---------------------------------------------------------------------------------------------
-// dK, dV: key-outer (128 keys per workgroup, 32 per wave) over 64-query tiles at or after the keys. Each tile runs as
-// two 32-query halves, the second half's S / dP MFMAs issued ahead of the first half's dV / dK MFMAs, which then run
-// beside the second half's elementwise work (with the dQ change: backward 584.3 -> 577.9 us, profiles/r4n/attn_ab.log).
+// dK, dV: key-outer (128 keys per workgroup, 32 per wave) over 64-query tiles at or after the keys. (The dQ kernel's
+// half-tile software pipeline did not pay here: 339 -> 361 us in the step at 240 VGPRs, profiles/r4o/summary.txt.)
 template <bool DROP>
 __global__ __launch_bounds__(64 * kDkdvWaves) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_bwd_dkdv_kernel(const bf16* __restrict__ qkv,
                                                                     const bf16* __restrict__ dout,
@@ -605,8 +604,12 @@ __global__ __launch_bounds__(64 * kDkdvWaves) __attribute__((amdgpu_waves_per_eu
     if (wave_valid && q0 + BQT - 1 >= k_lo) {  // wave-uniform: a query of the tile sees a key of the wave
       const bool diag = q0 < k_lo + 31;
       const uint32_t pre_t = DROP ? drop_pre(seed32(seed), ((uint32_t)bh * T + q0 + 4 * g) * (uint32_t)T + k_lo + (lane & 15)) : 0u;
-      // S / dP of 32-query half hq: s, dp [kg][fl] = S[q = q0 + 16(2hq+fl) + 4g + r][key = k_lo + 16kg + (l&15)]
-      auto sdp = [&](int hq, f32x4 (&s)[2][2], f32x4 (&dp)[2][2], f32x4 (&l4)[2], f32x4 (&d4)[2]) {
+      // Two 32-query halves per 64-query tile; each half is exactly one MFMA k-step of the dV/dK
+      // products, so only half of S / dP is live at a time (register pressure -> occupancy).
+#pragma unroll
+      for (int hq = 0; hq < 2; ++hq) {
+        f32x4 s[2][2], dp[2][2];  // [kg][fl]: S[q = q0 + 16(2hq+fl) + 4g + r][key = k_lo + 16kg + (l&15)]
+        f32x4 l4[2], d4[2];
 #pragma unroll
         for (int fl = 0; fl < 2; ++fl) {
           l4[fl] = *reinterpret_cast<const f32x4*>(Ls + 16 * (2 * hq + fl) + 4 * g);
@@ -615,6 +618,7 @@ __global__ __launch_bounds__(64 * kDkdvWaves) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
         for (int fl = 0; fl < 2; ++fl) {
           const int fi = 2 * hq + fl;
+          // dP' accumulates onto -delta (the rows' constants), so a kept entry's dP' - delta leaves the chain
           s[0][fl] = s[1][fl] = f32x4{0.f, 0.f, 0.f, 0.f};
           dp[0][fl] = dp[1][fl] = -d4[fl];
 #pragma unroll
@@ -628,66 +632,50 @@ __global__ __launch_bounds__(64 * kDkdvWaves) __attribute__((amdgpu_waves_per_eu
             }
           }
         }
-      };
-      // P, dS of half hq, packed: pk = {P_drop kg 0, P_drop kg 1, dS kg 0, dS kg 1}
-      auto elem = [&](auto diag_c, int hq, f32x4 (&s)[2][2], f32x4 (&dp)[2][2], const f32x4 (&l4)[2],
-                      const f32x4 (&d4)[2], bf16x8 (&pk)[4]) {
-        constexpr bool DIAG = decltype(diag_c)::value;
+        // P = exp2(S*scale*log2e - LSE*log2e); dropped entries: P_drop = 0 (dV; its 1/(1-p) is applied
+        // to dV at the end) and dP = 0 (dS); dP already carries 1/(1-p) through the prescaled V.
+        auto elementwise = [&](auto diag_c) {
+          constexpr bool DIAG = decltype(diag_c)::value;
 #pragma unroll
-        for (int kg = 0; kg < 2; ++kg) {
-          const int key = k_lo + 16 * kg + (lane & 15);
+          for (int kg = 0; kg < 2; ++kg) {
+            const int key = k_lo + 16 * kg + (lane & 15);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            uint32_t km[2] = {~0u, ~0u};
-            if constexpr (DROP)
-              drop_keep_masks(tk2, drop_fin(pre_t + ((uint32_t)(32 * hq + r) * (uint32_t)T + 16u * kg) * kDropC1,
-                                            seed_kx(seed)), km[0], km[1]);
+            for (int r = 0; r < 4; ++r) {
+              uint32_t km[2] = {~0u, ~0u};  // queries q and q^16 (fl = 0, 1) share one dropout hash
+              // counter (bh*T + q0 + 4g + 32hq + r) * T + key: a lane base plus (32hq + r) * T + 16kg (uniform)
+              if constexpr (DROP)
+                drop_keep_masks(tk2, drop_fin(pre_t + ((uint32_t)(32 * hq + r) * (uint32_t)T + 16u * kg) * kDropC1,
+                                              seed_kx(seed)), km[0], km[1]);
 #pragma unroll
-            for (int fl = 0; fl < 2; ++fl) {
-              float p = __builtin_amdgcn_exp2f(fmaf(s[kg][fl][r], sl2, -l4[fl][r]));
-              if constexpr (DIAG) p = (q0 + 16 * (2 * hq + fl) + 4 * g + r < key) ? 0.f : p;
-              float pdv = p, d = dp[kg][fl][r];
-              if constexpr (DROP) {
-                pdv = __uint_as_float(km[fl] & __float_as_uint(p));
-                d = sel_mask(km[fl], d, -d4[fl][r]);
+              for (int fl = 0; fl < 2; ++fl) {
+                float p = __builtin_amdgcn_exp2f(fmaf(s[kg][fl][r], sl2, -l4[fl][r]));
+                if constexpr (DIAG) p = (q0 + 16 * (2 * hq + fl) + 4 * g + r < key) ? 0.f : p;
+                float pdv = p, d = dp[kg][fl][r];  // dP' - delta
+                if constexpr (DROP) {
+                  pdv = __uint_as_float(km[fl] & __float_as_uint(p));
+                  d = sel_mask(km[fl], d, -d4[fl][r]);
+                }
+                dp[kg][fl][r] = pdv;  // dropped P (for dV)
+                s[kg][fl][r] = p * d;  // dS
               }
-              dp[kg][fl][r] = pdv;
-              s[kg][fl][r] = p * d;
             }
           }
-        }
-        pk[0] = pack_perm(dp[0], 0);
-        pk[1] = pack_perm(dp[1], 0);
-        pk[2] = pack_perm(s[0], 0);
-        pk[3] = pack_perm(s[1], 0);
-      };
-      auto dvdk = [&](int hq, const bf16x8 (&pk)[4]) {
+        };
+        if (diag) elementwise(std::true_type{});
+        else elementwise(std::false_type{});
+        const bf16x8 p0 = pack_perm(dp[0], 0), p1 = pack_perm(dp[1], 0);
+        const bf16x8 s0 = pack_perm(s[0], 0), s1 = pack_perm(s[1], 0);
 #pragma unroll
         for (int fd = 0; fd < 4; ++fd) {
           const bf16x8 dot = tr_frag(Ds, hq, 16 * fd, lane);
           const bf16x8 qt = tr_frag(Qs, hq, 16 * fd, lane);
-          dv[0][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dot, pk[0], dv[0][fd], 0, 0, 0);
-          dv[1][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dot, pk[1], dv[1][fd], 0, 0, 0);
-          dk[0][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qt, pk[2], dk[0][fd], 0, 0, 0);
-          dk[1][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qt, pk[3], dk[1][fd], 0, 0, 0);
+          dv[0][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dot, p0, dv[0][fd], 0, 0, 0);
+          dv[1][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dot, p1, dv[1][fd], 0, 0, 0);
+          dk[0][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qt, s0, dk[0][fd], 0, 0, 0);
+          dk[1][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qt, s1, dk[1][fd], 0, 0, 0);
         }
-      };
-      // half 0: S/dP, elementwise; half 1's S/dP issued next, then half 0's dV/dK beside half 1's elementwise
-      auto tile = [&](auto diag_c) {
-        f32x4 sa[2][2], dpa[2][2], la[2], da[2], sb[2][2], dpb[2][2], lb[2], db[2];
-        bf16x8 pa[4], pb[4];
-        sdp(0, sa, dpa, la, da);
-        elem(diag_c, 0, sa, dpa, la, da, pa);
-        sdp(1, sb, dpb, lb, db);
         __builtin_amdgcn_sched_barrier(0);
-        dvdk(0, pa);
-        elem(diag_c, 1, sb, dpb, lb, db, pb);
-        __builtin_amdgcn_sched_barrier(0);
-        dvdk(1, pb);
-        __builtin_amdgcn_sched_barrier(0);
-      };
-      if (diag) tile(std::true_type{});
-      else tile(std::false_type{});
+      }
     }
     if (i + 1 < nqt) sstore(smem + (cur ^ 1) * kStage);
     __syncthreads();
