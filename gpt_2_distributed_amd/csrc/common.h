@@ -119,12 +119,14 @@ __device__ __forceinline__ void drop_keep_masks(uint32_t tk2, uint32_t h, uint32
   m0 = (uint32_t)__builtin_amdgcn_sbfe((int)r, 15, 1);
   m1 = (uint32_t)((int)r >> 31);
 }
-// keep ? a : b for a lane mask m from drop_keep_masks: one v_bitop3_b32 (gfx950's 3-input bit operation, formed by
-// the compiler). Not inline asm: the compiler does not apply the MFMA-result read hazard (its wait states) to an asm
-// operand, and the attention backward feeds this select straight from MFMA accumulators — an asm v_bfi_b32 there read
-// stale dP values once the tile was software-pipelined (nondeterministic dK at p > 0, tools/attn_determinism.py)
+// keep ? a : b for a lane mask m from drop_keep_masks: one v_bitop3_b32 (gfx950's 3-input bit operation; truth table
+// 0xCA = S0 ? S1 : S2 bitwise) through its builtin. Not inline asm: the compiler does not apply the MFMA-result read
+// hazard (its wait states) to an asm operand, and the attention backward feeds this select straight from MFMA
+// accumulators — an asm v_bfi_b32 there read stale dP values once the dQ tile was software-pipelined
+// (nondeterministic dK at p > 0, tools/attn_determinism.py). Nor the C bit expression: in the kernels hipcc expands it
+// to 2-3 instructions (+156 per dK/dV tile body)
 __device__ __forceinline__ float sel_mask(uint32_t m, float a, float b) {
-  return __uint_as_float((m & __float_as_uint(a)) | (~m & __float_as_uint(b)));
+  return __uint_as_float(__builtin_amdgcn_bitop3_b32(m, __float_as_uint(a), __float_as_uint(b), 0xCA));
 }
 // element-indexed form: element i uses half (i & 1) of hash(i >> 1)
 __device__ __forceinline__ bool drop_keep(uint64_t seed, uint64_t idx, uint32_t thr) {
