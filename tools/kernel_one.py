@@ -13,8 +13,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from gpt_2_distributed_amd import _lib as K  # noqa: E402
 
 dev = "cuda"
-# the weight gradients as the engine launches them under autocast: bf16 split-K slabs (KERNEL_ONE_FP32_SLABS=1: fp32)
-SLABS = 0 if os.environ.get("KERNEL_ONE_FP32_SLABS") == "1" else K.SCHED_BF16_SLABS
+# the weight gradients as the engine launches them under autocast: fp32 split-K slabs since round 4
+# (Engine.WGRAD_BF16_SLABS = False; KERNEL_ONE_BF16_SLABS=1: the opt-in bf16 slabs)
+SLABS = K.SCHED_BF16_SLABS if os.environ.get("KERNEL_ONE_BF16_SLABS") == "1" else 0
 M, C, Vp, V, B, T, H = 65536, 768, 50432, 50257, 64, 1024, 12
 
 
