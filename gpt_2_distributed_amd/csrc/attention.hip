@@ -42,6 +42,12 @@ constexpr int BKV = 64;  // keys per K/V tile in fwd / dQ
 GPT2MI_PRODUCT_KNOB(ATTN_FWD_OCC, 3);
 GPT2MI_PRODUCT_KNOB(ATTN_FWD_LMAX, 1);
 GPT2MI_PRODUCT_KNOB(ATTN_DKDV_WAVES, 4);
+// dK/dV kernel: 0 = K / V fragments in registers, 64-query tiles (2 waves / SIMD); 1 = K / V rows of the workgroup in
+// LDS, 32-query tiles (a register budget for 3 waves / SIMD)
+#ifndef ATTN_DKDV_V3
+#define ATTN_DKDV_V3 0
+#endif
+GPT2MI_PRODUCT_KNOB(ATTN_DKDV_V3, 0);
 constexpr int kDkdvWaves = ATTN_DKDV_WAVES;  // waves per dK/dV workgroup (32 keys each)
 constexpr int BKB = 32 * kDkdvWaves;        // keys per workgroup in dK/dV
 constexpr int BQT = 64;  // queries per Q/dO tile in dK/dV
@@ -699,6 +705,187 @@ __global__ __launch_bounds__(64 * kDkdvWaves) __attribute__((amdgpu_waves_per_eu
   }
 }
 
+// dK, dV (v3): as attn_bwd_dkdv_kernel, with the workgroup's 128 keys' K and V rows in LDS (loaded once, V prescaled
+// by 1/(1-p)) instead of each wave's registers, and 32-query Q / dO tiles: the register budget of 3 waves / SIMD.
+constexpr int BQ3 = 32;
+template <bool DROP>
+__global__ __launch_bounds__(256, 3) void attn_bwd_dkdv3_kernel(const bf16* __restrict__ qkv,
+                                                                 const bf16* __restrict__ dout,
+                                                                 const float* __restrict__ lse,
+                                                                 const float* __restrict__ delta,
+                                                                 bf16* __restrict__ dqkv, float* __restrict__ csum,
+                                                                 int T, int H, float scale, uint64_t seed,
+                                                                 uint32_t thr, float inv_keep) {
+  constexpr int kKV = 128 * 128;            // [128 keys][64 d] bf16
+  constexpr int kTile = BQ3 * 128;          // [32 queries][64 d] bf16
+  constexpr int kStage = 2 * kTile + 2 * BQ3 * 4;  // Q, dO, lse, delta
+  __shared__ __attribute__((aligned(16))) char smem[2 * kKV + 2 * kStage];
+  char* const Kl = smem;
+  char* const Vl = smem + kKV;
+  char* const stg = smem + 2 * kKV;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
+  const int nqt = T / BQ3;
+  int bh, kb;
+  attn_block(bh, kb);
+  const int b = bh / H, h = bh % H;
+  const int C = H * D;
+  const size_t ld = 3 * (size_t)C;
+  const bf16* base = qkv + (size_t)b * T * ld;
+  const int k_lo = kb * 128 + 32 * w;
+  const bool wave_valid = k_lo < T;
+  // K and V rows kb*128 .. +128 (clamped to T - 1 past the end: only invalid waves read those) into LDS, swizzled as
+  // every tile (t_off); 4 chunks of 16 B per thread and array
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = threadIdx.x + 256 * i, row = idx >> 3, ch = idx & 7;
+    const size_t src = (size_t)min(kb * 128 + row, T - 1) * ld + h * D + 8 * ch;
+    const bf16x8 kv = *reinterpret_cast<const bf16x8*>(base + src + C);
+    bf16x8 vv = *reinterpret_cast<const bf16x8*>(base + src + 2 * C);
+    if (DROP) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) vv[e] = f2bf(bf2f(vv[e]) * inv_keep);
+    }
+    *reinterpret_cast<bf16x8*>(Kl + t_off(row, ch)) = kv;
+    *reinterpret_cast<bf16x8*>(Vl + t_off(row, ch)) = vv;
+  }
+  const float sl2 = scale * kLog2e;
+  [[maybe_unused]] const uint32_t tk2 = drop_tk2(thr > 0u ? thr : 1u);
+  f32x4 dk[2][4], dv[2][4];
+#pragma unroll
+  for (int kg = 0; kg < 2; ++kg)
+#pragma unroll
+    for (int f = 0; f < 4; ++f) dk[kg][f] = dv[kg][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const float* lrow = lse + (size_t)bh * T;
+  const float* drow = delta + (size_t)bh * T;
+  float rl = 0.f, rdl = 0.f;
+  const uint32_t qoff = tile_dma_off(ld, lane), doff = tile_dma_off(C, lane);
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const __amdgpu_buffer_rsrc_t rsq = qkv_rsrc(base), rsd = qkv_rsrc(dout + (size_t)b * T * C);
+  // Q / dO tiles (32 rows: one DMA instruction per wave and array); lse / delta by registers
+  auto gload = [&](int i, char* st) {
+    tile_dma<8>(st, rsq, i * BQ3, h * D, (int)ld, qoff, wu);
+    tile_dma<8>(st + kTile, rsd, i * BQ3, h * D, C, doff, wu);
+    if (threadIdx.x < BQ3) {
+      rl = lrow[i * BQ3 + threadIdx.x];
+      rdl = drow[i * BQ3 + threadIdx.x];
+    }
+  };
+  auto sstore = [&](char* st) {
+    if (threadIdx.x < BQ3) {
+      reinterpret_cast<float*>(st + 2 * kTile)[threadIdx.x] = rl * kLog2e;
+      reinterpret_cast<float*>(st + 2 * kTile + BQ3 * 4)[threadIdx.x] = rdl;
+    }
+  };
+  const int i0 = kb * 128 / BQ3;
+  gload(i0, stg);
+  sstore(stg);
+  __syncthreads();
+  const char* Kw = Kl + 32 * w * 128;  // this wave's 32 keys
+  const char* Vw = Vl + 32 * w * 128;
+  for (int i = i0; i < nqt; ++i) {
+    const int cur = (i - i0) & 1;
+    const char* Qs = stg + cur * kStage;
+    const char* Ds = Qs + kTile;
+    const float* Ls = reinterpret_cast<const float*>(Qs + 2 * kTile);
+    const float* Dl = Ls + BQ3;
+    if (i + 1 < nqt) gload(i + 1, stg + (cur ^ 1) * kStage);
+    const int q0 = i * BQ3;
+    if (wave_valid && q0 + BQ3 - 1 >= k_lo) {
+      const bool diag = q0 < k_lo + 31;
+      const uint32_t pre_t = DROP ? drop_pre(seed32(seed), ((uint32_t)bh * T + q0 + 4 * g) * (uint32_t)T + k_lo + (lane & 15)) : 0u;
+      f32x4 s[2][2], dp[2][2];  // [kg][fl]: S[q = q0 + 16fl + 4g + r][key = k_lo + 16kg + (l&15)]
+      f32x4 l4[2], d4[2];
+#pragma unroll
+      for (int fl = 0; fl < 2; ++fl) {
+        l4[fl] = *reinterpret_cast<const f32x4*>(Ls + 16 * fl + 4 * g);
+        d4[fl] = *reinterpret_cast<const f32x4*>(Dl + 16 * fl + 4 * g);
+        s[0][fl] = s[1][fl] = f32x4{0.f, 0.f, 0.f, 0.f};
+        dp[0][fl] = dp[1][fl] = -d4[fl];
+      }
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 kfr[2], vfr[2];
+#pragma unroll
+        for (int kg = 0; kg < 2; ++kg) {
+          kfr[kg] = row_frag(Kw, 16 * kg, kk, lane);
+          vfr[kg] = row_frag(Vw, 16 * kg, kk, lane);
+        }
+#pragma unroll
+        for (int fl = 0; fl < 2; ++fl) {
+          const bf16x8 qa = row_frag(Qs, 16 * fl, kk, lane);
+          const bf16x8 da = row_frag(Ds, 16 * fl, kk, lane);
+#pragma unroll
+          for (int kg = 0; kg < 2; ++kg) {
+            s[kg][fl] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kfr[kg], s[kg][fl], 0, 0, 0);
+            dp[kg][fl] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, vfr[kg], dp[kg][fl], 0, 0, 0);
+          }
+        }
+      }
+      auto elementwise = [&](auto diag_c) {
+        constexpr bool DIAG = decltype(diag_c)::value;
+#pragma unroll
+        for (int kg = 0; kg < 2; ++kg) {
+          const int key = k_lo + 16 * kg + (lane & 15);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            uint32_t km[2] = {~0u, ~0u};
+            if constexpr (DROP) {
+              uint32_t pv = pre_t;
+              asm volatile("" : "+v"(pv));  // hashed here, not hoisted ahead of the tile (its masks would not fit)
+              drop_keep_masks(tk2, drop_fin(pv + ((uint32_t)r * (uint32_t)T + 16u * kg) * kDropC1, seed_kx(seed)),
+                              km[0], km[1]);
+            }
+#pragma unroll
+            for (int fl = 0; fl < 2; ++fl) {
+              float p = __builtin_amdgcn_exp2f(fmaf(s[kg][fl][r], sl2, -l4[fl][r]));
+              if constexpr (DIAG) p = (q0 + 16 * fl + 4 * g + r < key) ? 0.f : p;
+              float pdv = p, d = dp[kg][fl][r];
+              if constexpr (DROP) {
+                pdv = __uint_as_float(km[fl] & __float_as_uint(p));
+                d = sel_mask(km[fl], d, -d4[fl][r]);
+              }
+              dp[kg][fl][r] = pdv;
+              s[kg][fl][r] = p * d;
+            }
+          }
+        }
+      };
+      if (diag) elementwise(std::true_type{});
+      else elementwise(std::false_type{});
+      const bf16x8 p0 = pack_perm(dp[0], 0), p1 = pack_perm(dp[1], 0);
+      const bf16x8 s0 = pack_perm(s[0], 0), s1 = pack_perm(s[1], 0);
+#pragma unroll
+      for (int fd = 0; fd < 4; ++fd) {
+        const bf16x8 dot = tr_frag(Ds, 0, 16 * fd, lane);
+        const bf16x8 qt = tr_frag(Qs, 0, 16 * fd, lane);
+        dv[0][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dot, p0, dv[0][fd], 0, 0, 0);
+        dv[1][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dot, p1, dv[1][fd], 0, 0, 0);
+        dk[0][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qt, s0, dk[0][fd], 0, 0, 0);
+        dk[1][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qt, s1, dk[1][fd], 0, 0, 0);
+      }
+    }
+    if (i + 1 < nqt) sstore(stg + (cur ^ 1) * kStage);
+    __syncthreads();
+  }
+  if (!wave_valid) return;
+#pragma unroll
+  for (int kg = 0; kg < 2; ++kg) {
+    const int key = k_lo + 16 * kg + (lane & 15);
+    bf16* kout = dqkv + ((size_t)b * T + key) * ld + C + h * D;
+    const f32x4 kv[4] = {dk[kg][0], dk[kg][1], dk[kg][2], dk[kg][3]};
+    const f32x4 vv[4] = {dv[kg][0], dv[kg][1], dv[kg][2], dv[kg][3]};
+    store_row64(kout, kv, scale, lane);
+    store_row64(kout + C, vv, DROP ? inv_keep : 1.f, lane);
+  }
+  if (csum) {
+    float* crow = csum + ((size_t)b * T + k_lo) / 32 * 3 * C + C + h * D + tile_colsum_col(lane);
+    const float ck = tile_colsum(dk, scale, lane);
+    const float cv = tile_colsum(dv, DROP ? inv_keep : 1.f, lane);
+    crow[0] = ck;
+    crow[C] = cv;
+  }
+}
+
 }  // namespace
 
 GPT2MI_EXPORT int gpt2mi_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int T, int H, int head_dim,
@@ -746,11 +933,21 @@ GPT2MI_EXPORT int gpt2mi_attn_bwd(const uint16_t* qkv, const uint16_t* out, cons
   int rc = gpt2mi::check_launch("attn_bwd_dq");
   if (rc) return rc;
   const dim3 gkv((T + BKB - 1) / BKB, B * H);
+#if ATTN_DKDV_V3
+  static_assert(BKB == 128, "the v3 dK/dV kernel assumes 128 keys per workgroup");
+  if (thr)
+    attn_bwd_dkdv3_kernel<true><<<gkv, 256, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta, (bf16*)dqkv,
+                                                    dqkv_colsum, T, H, scale, seed, thr, ik);
+  else
+    attn_bwd_dkdv3_kernel<false><<<gkv, 256, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta, (bf16*)dqkv,
+                                                     dqkv_colsum, T, H, scale, seed, thr, ik);
+#else
   if (thr)
     attn_bwd_dkdv_kernel<true><<<gkv, 64 * kDkdvWaves, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta,
                                                         (bf16*)dqkv, dqkv_colsum, T, H, scale, seed, thr, ik);
   else
     attn_bwd_dkdv_kernel<false><<<gkv, 64 * kDkdvWaves, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta,
                                                          (bf16*)dqkv, dqkv_colsum, T, H, scale, seed, thr, ik);
+#endif
   return gpt2mi::check_launch("attn_bwd_dkdv");
 }
