@@ -45,9 +45,9 @@ GPT2MI_PRODUCT_KNOB(ATTN_DKDV_WAVES, 4);
 // dK/dV kernel: 0 = K / V fragments in registers, 64-query tiles (2 waves / SIMD); 1 = K / V rows of the workgroup in
 // LDS, 32-query tiles (a register budget for 3 waves / SIMD)
 #ifndef ATTN_DKDV_V3
-#define ATTN_DKDV_V3 0
+#define ATTN_DKDV_V3 1
 #endif
-GPT2MI_PRODUCT_KNOB(ATTN_DKDV_V3, 0);
+GPT2MI_PRODUCT_KNOB(ATTN_DKDV_V3, 1);
 constexpr int kDkdvWaves = ATTN_DKDV_WAVES;  // waves per dK/dV workgroup (32 keys each)
 constexpr int BKB = 32 * kDkdvWaves;        // keys per workgroup in dK/dV
 constexpr int BQT = 64;  // queries per Q/dO tile in dK/dV
