@@ -36,21 +36,9 @@ constexpr int BKV = 64;  // keys per K/V tile in fwd / dQ
 #ifndef ATTN_FWD_LMAX
 #define ATTN_FWD_LMAX 1  // forward rescale test on each lane's own scores (0: cross-lane max every tile, A/B builds)
 #endif
-#ifndef ATTN_DKDV_WAVES
-#define ATTN_DKDV_WAVES 4
-#endif
 GPT2MI_PRODUCT_KNOB(ATTN_FWD_OCC, 3);
 GPT2MI_PRODUCT_KNOB(ATTN_FWD_LMAX, 1);
-GPT2MI_PRODUCT_KNOB(ATTN_DKDV_WAVES, 4);
-// dK/dV kernel: 0 = K / V fragments in registers, 64-query tiles (2 waves / SIMD); 1 = K / V rows of the workgroup in
-// LDS, 32-query tiles (a register budget for 3 waves / SIMD)
-#ifndef ATTN_DKDV_V3
-#define ATTN_DKDV_V3 1
-#endif
-GPT2MI_PRODUCT_KNOB(ATTN_DKDV_V3, 1);
-constexpr int kDkdvWaves = ATTN_DKDV_WAVES;  // waves per dK/dV workgroup (32 keys each)
-constexpr int BKB = 32 * kDkdvWaves;        // keys per workgroup in dK/dV
-constexpr int BQT = 64;  // queries per Q/dO tile in dK/dV
+constexpr int BKB = 128;  // keys per workgroup in dK/dV (4 waves of 32)
 constexpr int kThreads = 256;
 constexpr float kLog2e = 1.4426950408889634f;
 
@@ -530,193 +518,20 @@ __global__ __launch_bounds__(kThreads, 3) void attn_bwd_dq_kernel(const bf16* __
 }
 
 // ---------------------------------------------------------------------------------------------
-// dK, dV: key-outer (128 keys per workgroup, 32 per wave) over 64-query tiles at or after the keys. (The dQ kernel's
-// half-tile software pipeline did not pay here: 339 -> 361 us in the step at 240 VGPRs, profiles/r4o/summary.txt.)
-template <bool DROP>
-__global__ __launch_bounds__(64 * kDkdvWaves) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_bwd_dkdv_kernel(const bf16* __restrict__ qkv,
-                                                                    const bf16* __restrict__ dout,
-                                                                    const float* __restrict__ lse,
-                                                                    const float* __restrict__ delta,
-                                                                    bf16* __restrict__ dqkv, float* __restrict__ csum,
-                                                                    int T, int H, float scale, uint64_t seed,
-                                                                    uint32_t thr, float inv_keep) {
-  constexpr int kTile = BQT * 128;
-  constexpr int kStage = 2 * kTile + 2 * BQT * 4;
-  __shared__ __attribute__((aligned(16))) char smem[2 * kStage];  // 2 x (Q, dO, lse, delta)
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
-  const int nqt = T / BQT;
-  int bh, kb;  // kb: key block (heaviest first)
-  attn_block(bh, kb);
-  const int b = bh / H, h = bh % H;
-  const int C = H * D;
-  const size_t ld = 3 * (size_t)C;
-  const bf16* base = qkv + (size_t)b * T * ld;
-  const int k_lo = kb * BKB + 32 * w;  // first key of this wave
-  const bool wave_valid = k_lo < T;
-  bf16x8 kf[2][2], vf[2][2];
-#pragma unroll
-  for (int kg = 0; kg < 2; ++kg)
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const size_t row = (size_t)min(k_lo + 16 * kg + (lane & 15), T - 1) * ld;
-      kf[kg][kk] = *reinterpret_cast<const bf16x8*>(base + row + C + h * D + 32 * kk + 8 * g);
-      vf[kg][kk] = *reinterpret_cast<const bf16x8*>(base + row + 2 * C + h * D + 32 * kk + 8 * g);
-      if (DROP) {  // dP' = dO.(V/(1-p)): the keep-scale of dropout folded into V once per wave
-#pragma unroll
-        for (int e = 0; e < 8; ++e) vf[kg][kk][e] = f2bf(bf2f(vf[kg][kk][e]) * inv_keep);
-      }
-    }
-  const float sl2 = scale * kLog2e;
-  [[maybe_unused]] const uint32_t tk2 = drop_tk2(thr > 0u ? thr : 1u);
-  f32x4 dk[2][4], dv[2][4];
-#pragma unroll
-  for (int kg = 0; kg < 2; ++kg)
-#pragma unroll
-    for (int f = 0; f < 4; ++f) dk[kg][f] = dv[kg][f] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const float* lrow = lse + (size_t)bh * T;
-  const float* drow = delta + (size_t)bh * T;
-
-  float rl = 0.f, rdl = 0.f;
-  const uint32_t qoff = tile_dma_off(ld, lane), doff = tile_dma_off(C, lane);
-  const int wu = __builtin_amdgcn_readfirstlane(w);
-  const __amdgpu_buffer_rsrc_t rsq = qkv_rsrc(base), rsd = qkv_rsrc(dout + (size_t)b * T * C);
-  // Q / dO tiles by LDS-DMA straight into stage `st`; lse / delta by registers (scaled at their LDS write)
-  auto gload = [&](int i, char* st) {
-    tile_dma<kDkdvWaves>(st, rsq, i * BQT, h * D, (int)ld, qoff, wu);
-    tile_dma<kDkdvWaves>(st + kTile, rsd, i * BQT, h * D, C, doff, wu);
-    if (threadIdx.x < BQT) {  // raw values: any use here would wait (in-order vmcnt) for the tiles above too
-      rl = lrow[i * BQT + threadIdx.x];
-      rdl = drow[i * BQT + threadIdx.x];
-    }
-  };
-  auto sstore = [&](char* st) {
-    if (threadIdx.x < BQT) {
-      reinterpret_cast<float*>(st + 2 * kTile)[threadIdx.x] = rl * kLog2e;
-      reinterpret_cast<float*>(st + 2 * kTile + BQT * 4)[threadIdx.x] = rdl;
-    }
-  };
-  const int i0 = kb * BKB / BQT;
-  gload(i0, smem);
-  sstore(smem);
-  __syncthreads();
-  for (int i = i0; i < nqt; ++i) {
-    const int cur = (i - i0) & 1;
-    const char* Qs = smem + cur * kStage;
-    const char* Ds = Qs + kTile;
-    const float* Ls = reinterpret_cast<const float*>(Qs + 2 * kTile);
-    const float* Dl = Ls + BQT;
-    if (i + 1 < nqt) gload(i + 1, smem + (cur ^ 1) * kStage);
-    const int q0 = i * BQT;
-    if (wave_valid && q0 + BQT - 1 >= k_lo) {  // wave-uniform: a query of the tile sees a key of the wave
-      const bool diag = q0 < k_lo + 31;
-      const uint32_t pre_t = DROP ? drop_pre(seed32(seed), ((uint32_t)bh * T + q0 + 4 * g) * (uint32_t)T + k_lo + (lane & 15)) : 0u;
-      // Two 32-query halves per 64-query tile; each half is exactly one MFMA k-step of the dV/dK
-      // products, so only half of S / dP is live at a time (register pressure -> occupancy).
-#pragma unroll
-      for (int hq = 0; hq < 2; ++hq) {
-        f32x4 s[2][2], dp[2][2];  // [kg][fl]: S[q = q0 + 16(2hq+fl) + 4g + r][key = k_lo + 16kg + (l&15)]
-        f32x4 l4[2], d4[2];
-#pragma unroll
-        for (int fl = 0; fl < 2; ++fl) {
-          l4[fl] = *reinterpret_cast<const f32x4*>(Ls + 16 * (2 * hq + fl) + 4 * g);
-          d4[fl] = *reinterpret_cast<const f32x4*>(Dl + 16 * (2 * hq + fl) + 4 * g);
-        }
-#pragma unroll
-        for (int fl = 0; fl < 2; ++fl) {
-          const int fi = 2 * hq + fl;
-          // dP' accumulates onto -delta (the rows' constants), so a kept entry's dP' - delta leaves the chain
-          s[0][fl] = s[1][fl] = f32x4{0.f, 0.f, 0.f, 0.f};
-          dp[0][fl] = dp[1][fl] = -d4[fl];
-#pragma unroll
-          for (int kk = 0; kk < 2; ++kk) {
-            const bf16x8 qa = row_frag(Qs, 16 * fi, kk, lane);
-            const bf16x8 da = row_frag(Ds, 16 * fi, kk, lane);
-#pragma unroll
-            for (int kg = 0; kg < 2; ++kg) {
-              s[kg][fl] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[kg][kk], s[kg][fl], 0, 0, 0);
-              dp[kg][fl] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, vf[kg][kk], dp[kg][fl], 0, 0, 0);
-            }
-          }
-        }
-        // P = exp2(S*scale*log2e - LSE*log2e); dropped entries: P_drop = 0 (dV; its 1/(1-p) is applied
-        // to dV at the end) and dP = 0 (dS); dP already carries 1/(1-p) through the prescaled V.
-        auto elementwise = [&](auto diag_c) {
-          constexpr bool DIAG = decltype(diag_c)::value;
-#pragma unroll
-          for (int kg = 0; kg < 2; ++kg) {
-            const int key = k_lo + 16 * kg + (lane & 15);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              uint32_t km[2] = {~0u, ~0u};  // queries q and q^16 (fl = 0, 1) share one dropout hash
-              // counter (bh*T + q0 + 4g + 32hq + r) * T + key: a lane base plus (32hq + r) * T + 16kg (uniform)
-              if constexpr (DROP)
-                drop_keep_masks(tk2, drop_fin(pre_t + ((uint32_t)(32 * hq + r) * (uint32_t)T + 16u * kg) * kDropC1,
-                                              seed_kx(seed)), km[0], km[1]);
-#pragma unroll
-              for (int fl = 0; fl < 2; ++fl) {
-                float p = __builtin_amdgcn_exp2f(fmaf(s[kg][fl][r], sl2, -l4[fl][r]));
-                if constexpr (DIAG) p = (q0 + 16 * (2 * hq + fl) + 4 * g + r < key) ? 0.f : p;
-                float pdv = p, d = dp[kg][fl][r];  // dP' - delta
-                if constexpr (DROP) {
-                  pdv = __uint_as_float(km[fl] & __float_as_uint(p));
-                  d = sel_mask(km[fl], d, -d4[fl][r]);
-                }
-                dp[kg][fl][r] = pdv;  // dropped P (for dV)
-                s[kg][fl][r] = p * d;  // dS
-              }
-            }
-          }
-        };
-        if (diag) elementwise(std::true_type{});
-        else elementwise(std::false_type{});
-        const bf16x8 p0 = pack_perm(dp[0], 0), p1 = pack_perm(dp[1], 0);
-        const bf16x8 s0 = pack_perm(s[0], 0), s1 = pack_perm(s[1], 0);
-#pragma unroll
-        for (int fd = 0; fd < 4; ++fd) {
-          const bf16x8 dot = tr_frag(Ds, hq, 16 * fd, lane);
-          const bf16x8 qt = tr_frag(Qs, hq, 16 * fd, lane);
-          dv[0][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dot, p0, dv[0][fd], 0, 0, 0);
-          dv[1][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dot, p1, dv[1][fd], 0, 0, 0);
-          dk[0][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qt, s0, dk[0][fd], 0, 0, 0);
-          dk[1][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qt, s1, dk[1][fd], 0, 0, 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    if (i + 1 < nqt) sstore(smem + (cur ^ 1) * kStage);
-    __syncthreads();
-  }
-  if (!wave_valid) return;
-#pragma unroll
-  for (int kg = 0; kg < 2; ++kg) {
-    const int key = k_lo + 16 * kg + (lane & 15);
-    bf16* kout = dqkv + ((size_t)b * T + key) * ld + C + h * D;
-    const f32x4 kv[4] = {dk[kg][0], dk[kg][1], dk[kg][2], dk[kg][3]};
-    const f32x4 vv[4] = {dv[kg][0], dv[kg][1], dv[kg][2], dv[kg][3]};
-    store_row64(kout, kv, scale, lane);
-    store_row64(kout + C, vv, DROP ? inv_keep : 1.f, lane);
-  }
-  if (csum) {  // partial qkv-bias gradient: row (b*T + k_lo)/32 of csum [B*T/32][3C], k and v columns
-    float* crow = csum + ((size_t)b * T + k_lo) / 32 * 3 * C + C + h * D + tile_colsum_col(lane);
-    const float ck = tile_colsum(dk, scale, lane);
-    const float cv = tile_colsum(dv, DROP ? inv_keep : 1.f, lane);
-    crow[0] = ck;
-    crow[C] = cv;
-  }
-}
-
-// dK, dV (v3): as attn_bwd_dkdv_kernel, with the workgroup's 128 keys' K and V rows in LDS (loaded once, V prescaled
-// by 1/(1-p)) instead of each wave's registers, and 32-query Q / dO tiles: the register budget of 3 waves / SIMD.
+// dK, dV: key-outer (128 keys per workgroup, 32 per wave) over 32-query Q / dO tiles at or after the keys. The
+// workgroup's K and V rows live in LDS (loaded once, V prescaled by 1/(1-p)) and the waves read their fragments per
+// tile, instead of holding them in registers: 166 VGPRs, 3 waves / SIMD (the round-3 kernel held K / V in 32 VGPRs
+// and took 64-query tiles at 224 VGPRs, 2 waves / SIMD: 339-354 -> 315 us per layer in the step, profiles/r4s/).
 constexpr int BQ3 = 32;
 template <bool DROP>
-__global__ __launch_bounds__(256, 3) void attn_bwd_dkdv3_kernel(const bf16* __restrict__ qkv,
+__global__ __launch_bounds__(256, 3) void attn_bwd_dkdv_kernel(const bf16* __restrict__ qkv,
                                                                  const bf16* __restrict__ dout,
                                                                  const float* __restrict__ lse,
                                                                  const float* __restrict__ delta,
                                                                  bf16* __restrict__ dqkv, float* __restrict__ csum,
                                                                  int T, int H, float scale, uint64_t seed,
                                                                  uint32_t thr, float inv_keep) {
-  constexpr int kKV = 128 * 128;            // [128 keys][64 d] bf16
+  constexpr int kKV = BKB * 128;            // [128 keys][64 d] bf16
   constexpr int kTile = BQ3 * 128;          // [32 queries][64 d] bf16
   constexpr int kStage = 2 * kTile + 2 * BQ3 * 4;  // Q, dO, lse, delta
   __shared__ __attribute__((aligned(16))) char smem[2 * kKV + 2 * kStage];
@@ -933,21 +748,11 @@ GPT2MI_EXPORT int gpt2mi_attn_bwd(const uint16_t* qkv, const uint16_t* out, cons
   int rc = gpt2mi::check_launch("attn_bwd_dq");
   if (rc) return rc;
   const dim3 gkv((T + BKB - 1) / BKB, B * H);
-#if ATTN_DKDV_V3
-  static_assert(BKB == 128, "the v3 dK/dV kernel assumes 128 keys per workgroup");
   if (thr)
-    attn_bwd_dkdv3_kernel<true><<<gkv, 256, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta, (bf16*)dqkv,
+    attn_bwd_dkdv_kernel<true><<<gkv, 256, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta, (bf16*)dqkv,
                                                     dqkv_colsum, T, H, scale, seed, thr, ik);
   else
-    attn_bwd_dkdv3_kernel<false><<<gkv, 256, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta, (bf16*)dqkv,
+    attn_bwd_dkdv_kernel<false><<<gkv, 256, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta, (bf16*)dqkv,
                                                      dqkv_colsum, T, H, scale, seed, thr, ik);
-#else
-  if (thr)
-    attn_bwd_dkdv_kernel<true><<<gkv, 64 * kDkdvWaves, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta,
-                                                        (bf16*)dqkv, dqkv_colsum, T, H, scale, seed, thr, ik);
-  else
-    attn_bwd_dkdv_kernel<false><<<gkv, 64 * kDkdvWaves, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse, delta,
-                                                         (bf16*)dqkv, dqkv_colsum, T, H, scale, seed, thr, ik);
-#endif
   return gpt2mi::check_launch("attn_bwd_dkdv");
 }

@@ -17,7 +17,7 @@ HIPCC = "/opt/rocm/bin/hipcc"
 # source -> {kernel-name substring: minimum occupancy (waves/SIMD)}
 EXPECT = {
     "gemm_pp.hip": {"gemm_pp_kernel": 2},
-    "attention.hip": {"attn_fwd_kernel": 3, "attn_bwd_dkdv": 2, "attn_bwd_dq_kernel": 3},
+    "attention.hip": {"attn_fwd_kernel": 3, "attn_bwd_dkdv_kernel": 3, "attn_bwd_dq_kernel": 3},
 }
 
 
