@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("GPT2MI_LIB") or os.path.join(_HERE, "libgpt2mi.so")
 
 # the ABI these bindings are written against (include/gpt2mi.h GPT2MI_ABI_VERSION): a stale or foreign
 # library is refused at load instead of being called with the wrong argument lists
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 _c_int, _c_float, _c_size, _c_u64, _p = ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_void_p
 
@@ -39,6 +39,7 @@ _SIGS = {
     "gpt2mi_adamw": [_p, _p, _p, _p, _p, _c_size, _c_float, _c_float, _c_float, _c_float, _c_float, _c_int,
                      _c_float, _p, _p, _p],
     "gpt2mi_grad_norm": [_p, _c_size, _c_float, _p, _p, _p],
+    "gpt2mi_norm_finalize": [_p, _c_int, _p, _p],
     "gpt2mi_norm_partials_size": [],
     "gpt2mi_cast_f32_bf16": [_p, _p, _c_size, _p],
     "gpt2mi_transpose_bf16": [_p, _p, _c_int, _c_int, _c_int, _c_int, _p],
@@ -238,6 +239,11 @@ def adamw(p, g, m, v, p_bf16, n, lr, wd, b1, b2, eps, step, grad_scale, partials
 
 def grad_norm(g, n, scale, partials, out):
     _call("gpt2mi_grad_norm", _ptr(g), n, scale, _ptr(partials), _ptr(out), _stream())
+
+
+def norm_finalize(partials, n, out):
+    """out[0] = sqrt(sum(partials[:n])) (the norm of adamw launches given grad_norm=None)."""
+    _call("gpt2mi_norm_finalize", _ptr(partials), n, _ptr(out), _stream())
 
 
 def norm_partials_size() -> int:

@@ -403,6 +403,12 @@ GPT2MI_EXPORT int gpt2mi_grad_norm(const float* g, size_t n, float scale, float*
 
 GPT2MI_EXPORT int gpt2mi_norm_partials_size(void) { return kNormBlocks; }
 
+GPT2MI_EXPORT int gpt2mi_norm_finalize(const float* partials, int n, float* out, void* stream) {
+  GPT2MI_REQUIRE(n > 0, "norm_finalize: n=%d", n);
+  norm_finalize_kernel<<<1, 256, 0, (hipStream_t)stream>>>(partials, n, out);
+  return gpt2mi::check_launch("norm_finalize");
+}
+
 GPT2MI_EXPORT int gpt2mi_cast_f32_bf16(const float* x, uint16_t* y, size_t n, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   cast_f32_bf16_kernel<<<2048, 256, 0, s>>>(x, (bf16*)y, n);

@@ -34,14 +34,16 @@ class _FlatAdamW(torch.optim.Optimizer):
         self.step_count = 0
         self.grad_scale = 1.0
 
-    def _run(self, p, g, pb, lo=0, hi=None, grad_norm=None):
-        """One fused AdamW launch over p[lo:hi] (step_count advanced by the caller)."""
+    def _run(self, p, g, pb, lo=0, hi=None, partials=None):
+        """One fused AdamW launch over p[lo:hi] (step_count advanced by the caller). partials: the grad-norm partial
+        sums go there and the norm is left to the caller (gpt2mi_norm_finalize); else self.grad_norm is written."""
         grp = self.param_groups[0]
         b1, b2 = grp["betas"]
         hi = p.numel() if hi is None else hi
         K.adamw(p[lo:hi], g[lo:hi], self.exp_avg[lo:hi], self.exp_avg_sq[lo:hi], pb, hi - lo, float(grp["lr"]),
                 float(grp["weight_decay"]), float(b1), float(b2), float(grp["eps"]), self.step_count,
-                float(self.grad_scale), self.partials, self.grad_norm if grad_norm is None else grad_norm)
+                float(self.grad_scale), self.partials if partials is None else partials,
+                self.grad_norm if partials is None else None)
 
     def state_dict(self):
         return {"step": self.step_count, "exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq,
@@ -91,13 +93,14 @@ class FusedAdamW(_FlatAdamW):
 
 class ShardedAdamW(_FlatAdamW):
     """One launch per FSDP unit: each writes its unit's bf16 shard straight into that unit's all-gather buffer
-    (FullyShardedDataParallel.bf16_chunk), so the next forward gathers in place; the units' grad norms are combined
-    into the clip_grad_norm_ value."""
+    (FullyShardedDataParallel.bf16_chunk), so the next forward gathers in place, and its grad-norm partial sums into
+    its slice of one buffer, finalised once into the clip_grad_norm_ value."""
 
     def __init__(self, fsdp, lr=1e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1):
         super().__init__([fsdp.flat_param], fsdp.flat_param, lr, betas, eps, weight_decay)
         self.fsdp = fsdp
-        self.unit_norms = torch.zeros(len(fsdp.plans), dtype=torch.float32, device=fsdp.flat_param.device)
+        self.unit_partials = torch.empty(len(fsdp.plans) * K.norm_partials_size(), dtype=torch.float32,
+                                         device=fsdp.flat_param.device)
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -110,14 +113,16 @@ class ShardedAdamW(_FlatAdamW):
             return loss  # no backward since zero_grad(set_to_none=True): skipped, as torch's optimizers do
         self.step_count += 1
         p = f.flat_param.detach()
+        P = K.norm_partials_size()
         for i, q in enumerate(f.plans):
-            self._run(p, f.grad_shard, f.bf16_chunk(q.name), q.soff, q.soff + q.per, self.unit_norms[i:i + 1])
+            self._run(p, f.grad_shard, f.bf16_chunk(q.name), q.soff, q.soff + q.per, self.unit_partials[i * P:(i + 1) * P])
         f.mark_params_updated(bf16_fresh=True)
-        # the clip_grad_norm_(inf) value of the full model: sum of squares over units (and shards)
-        n2 = self.unit_norms.square().sum(0, keepdim=True)
+        # the clip_grad_norm_(inf) value of the full model: sum of squares over units (one finalisation) and shards
+        K.norm_finalize(self.unit_partials, self.unit_partials.numel(), self.grad_norm)
         if f.coll:
+            n2 = self.grad_norm.square()
             dist.all_reduce(n2)
-        torch.sqrt(n2, out=self.grad_norm)
+            torch.sqrt(n2, out=self.grad_norm)
         return loss
 
     def zero_grad(self, set_to_none: bool = True):

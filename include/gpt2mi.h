@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GPT2MI_ABI_VERSION 11
+#define GPT2MI_ABI_VERSION 12
 
 const char* gpt2mi_last_error(void);
 int gpt2mi_abi_version(void); /* returns GPT2MI_ABI_VERSION of the built library */
@@ -139,6 +139,9 @@ int gpt2mi_adamw(float* p, const float* g, float* m, float* v, uint16_t* p_bf16,
                  float b1, float b2, float eps, int step, float grad_scale, float* partials, float* grad_norm,
                  void* stream);
 int gpt2mi_grad_norm(const float* g, size_t n, float scale, float* partials, float* out, void* stream);
+/* v12: out[0] = sqrt(sum of partials[0..n)) — the norm of several gpt2mi_adamw launches given grad_norm = NULL and
+ * consecutive gpt2mi_norm_partials_size()-float slices of one partials buffer (FSDP's AdamW runs once per unit). */
+int gpt2mi_norm_finalize(const float* partials, int n, float* out, void* stream);
 int gpt2mi_norm_partials_size(void);
 
 /* ---- fp32 mode: the reference model.py run WITHOUT torch.autocast (plain fp32 module; the CPU

@@ -436,6 +436,33 @@ def test_adamw_matches_oracle_and_norm(n):
     assert abs(gn.item() - gr.norm().item()) < 1e-5 * gr.norm().item()
 
 
+def test_adamw_in_pieces_with_one_norm_finalisation():
+    """FSDP's AdamW (optim.ShardedAdamW): one launch per unit range with grad_norm = NULL, each writing its partial sums
+    into its slice of one buffer, then gpt2mi_norm_finalize over all slices: the same parameters as one launch over
+    the whole range and the whole range's grad norm."""
+    n, cuts = 3 * 4096 + 64, [0, 4096, 4160, 3 * 4096 + 64]
+    g = torch.Generator().manual_seed(12)
+    p0, gr = torch.randn(n, generator=g).to(dev), (torch.randn(n, generator=g) * 0.01).to(dev)
+    P = L().norm_partials_size()
+    outs = []
+    for pieces in (False, True):
+        p, m, v = p0.clone(), torch.zeros(n, device=dev), torch.zeros(n, device=dev)
+        pb = torch.empty(n, dtype=torch.bfloat16, device=dev)
+        gn = torch.empty(1, device=dev)
+        part = torch.empty(3 * P, device=dev)
+        if pieces:
+            for i, (a, b) in enumerate(zip(cuts, cuts[1:])):
+                L().adamw(p[a:b], gr[a:b], m[a:b], v[a:b], pb[a:b], b - a, 1e-3, 0.1, 0.9, 0.95, 1e-8, 1, 1.0,
+                          part[i * P:(i + 1) * P], None)
+            L().norm_finalize(part, 3 * P, gn)
+        else:
+            L().adamw(p, gr, m, v, pb, n, 1e-3, 0.1, 0.9, 0.95, 1e-8, 1, 1.0, part, gn)
+        outs.append((p, pb, gn))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    assert abs(outs[1][2].item() - gr.norm().item()) < 1e-5 * gr.norm().item()
+
+
 def test_colsum():
     M, N = 1000, 2304
     g = bf(torch.randn(M, N))
