@@ -258,28 +258,9 @@ int launch(const GemmParams& P, hipStream_t s, int splits) {
 // out[i] (+)= sum_z slab[z][i]   (fixed summation order: deterministic). The slabs' loads go out in groups of 8 before
 // their adds (in split order: the same bits as one load per add), so a thread keeps 8 loads in flight instead of one
 // (the 27-split proj reduction was latency-bound)
-#ifndef SPLITK_REDUCE_EXP
-#define SPLITK_REDUCE_EXP 0
-#endif
-GPT2MI_PRODUCT_KNOB(SPLITK_REDUCE_EXP, 0);
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ slab, int splits, size_t n4,
                                                             float* __restrict__ out, int accumulate) {
   const f32x4* s4 = reinterpret_cast<const f32x4*>(slab);
-#if SPLITK_REDUCE_EXP == 1
-  // A/B: every slab load of the element issued before the first add (up to 32 in flight), same order of adds
-  for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
-    f32x4 s = accumulate ? reinterpret_cast<const f32x4*>(out)[i] : f32x4{0.f, 0.f, 0.f, 0.f};
-    f32x4 v[32];
-#pragma unroll
-    for (int u = 0; u < 32; ++u)
-      if (u < splits) v[u] = s4[(size_t)u * n4 + i];
-#pragma unroll
-    for (int u = 0; u < 32; ++u)
-      if (u < splits) s += v[u];
-    for (int z = 32; z < splits; ++z) s += s4[(size_t)z * n4 + i];
-    reinterpret_cast<f32x4*>(out)[i] = s;
-  }
-#else
   for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
     f32x4 s = accumulate ? reinterpret_cast<const f32x4*>(out)[i] : f32x4{0.f, 0.f, 0.f, 0.f};
     for (int z = 0; z < splits; z += 8) {
@@ -294,7 +275,6 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
     }
     reinterpret_cast<f32x4*>(out)[i] = s;
   }
-#endif
 }
 
 // bf16 slabs (GPT2MI_SCHED_BF16_SLABS): 8 elements per thread (one 16-B load per slab), each widened to fp32 and added
@@ -400,12 +380,7 @@ int splitk_reduce16(const bf16* slab, int splits, size_t n, float* out, int accu
   return check_launch("splitk_reduce16");
 }
 int splitk_reduce(const float* slab, int splits, size_t n, float* out, int accumulate, hipStream_t s) {
-#if SPLITK_REDUCE_EXP == 2
-  // A/B: one thread per float4 (the grid covers n / 4 once: no grid-stride loop, every thread's loads at once)
-  splitk_reduce_kernel<<<(unsigned)((n / 4 + 255) / 256), 256, 0, s>>>(slab, splits, n / 4, out, accumulate);
-#else
   splitk_reduce_kernel<<<2048, 256, 0, s>>>(slab, splits, n / 4, out, accumulate);
-#endif
   return check_launch("splitk_reduce");
 }
 }  // namespace gpt2mi
