@@ -150,6 +150,13 @@ def gemm_mode(libs, g, st):
     stag = [v for v in os.environ.get("LIB_AB_STAGGER", "").split(";") if v]
     ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
     dbs = {name: torch.zeros(v[1], device=dev) for name, v in data.items() if v[6] == K.EPI_GELU_BWD}
+    # LIB_AB_HOG=<blocks>: every timed batch runs beside tools/ab/libhog.so's CU hog (that many CUs held for 3 ms on a
+    # side stream, as RCCL kernels hold them in a data-parallel step)
+    hog_blocks = int(os.environ.get("LIB_AB_HOG", "0"))
+    if hog_blocks:
+        hog = ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "ab", "libhog.so"))
+        hog.hog.argtypes = [ctypes.c_int, ctypes.c_longlong, ctypes.c_void_p]
+        side = torch.cuda.Stream()
     for _ in range(5):
         for name, (lay, n, k, A, B, out, epi, bias, resid, aux) in data.items():
             ldb = k if lay == 0 else n
@@ -162,6 +169,9 @@ def gemm_mode(libs, g, st):
                                              1.0, None, 0, 1, pd, 5, ptr(dbs.get(name)), _sched(lib), st)
                 assert fn() == 0
                 s, e = ev(), ev()
+                if hog_blocks:
+                    torch.cuda.synchronize()
+                    assert hog.hog(hog_blocks, 3_000_000, side.cuda_stream) == 0
                 s.record()
                 for _r in range(5):
                     fn()
