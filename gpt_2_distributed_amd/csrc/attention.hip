@@ -136,6 +136,12 @@ __device__ __forceinline__ void store_row64(bf16* row, const f32x4 (&v)[4], floa
 }
 
 constexpr float kRescaleThr = 8.f;  // log2 units: P <= 256 between rescales (bf16-exact exponent range)
+// exp2(a x + b) of a pair: the affine part as ONE packed FMA (v_pk_fma_f32, two lanes' worth per issue; each component
+// the same fused fma as fmaf, so the same bits), the exponentials one by one (no packed transcendental)
+__device__ __forceinline__ f32x2 exp2_affine2(float x0, float x1, float a, float b) {
+  const f32x2 t = __builtin_elementwise_fma(f32x2{x0, x1}, f32x2{a, a}, f32x2{b, b});
+  return f32x2{__builtin_amdgcn_exp2f(t[0]), __builtin_amdgcn_exp2f(t[1])};
+}
 
 // pack accumulator registers acc[2kk + (j>>2)][j&3] (j = 0..7) to a bf16 operand fragment
 __device__ __forceinline__ bf16x8 pack_perm(const f32x4* acc, int kk) {
@@ -304,7 +310,11 @@ __global__ __launch_bounds__(kThreads, ATTN_FWD_OCC) void attn_fwd_kernel(const 
 #pragma unroll
         for (int fi = 0; fi < 4; ++fi)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) s[qg][fi][r] = __builtin_amdgcn_exp2f(fmaf(s[qg][fi][r], sl2, -m[qg]));
+          for (int r = 0; r < 4; r += 2) {
+            const f32x2 e = exp2_affine2(s[qg][fi][r], s[qg][fi][r + 1], sl2, -m[qg]);
+            s[qg][fi][r] = e[0];
+            s[qg][fi][r + 1] = e[1];
+          }
       }
       // P packed to bf16 once per 32-key half (kk): the row sums (before dropout: the normaliser is the undropped
       // softmax denominator) and P.V read the same fragments. Dropout on the packed P (its 1/(1-p) goes into the
@@ -462,17 +472,26 @@ __global__ __launch_bounds__(kThreads, 3) void attn_bwd_dq_kernel(const bf16* __
         for (int f = 0; f < 2; ++f) {
           const int fi = 2 * kk + f;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            uint32_t km[2] = {~0u, ~0u};
-            if constexpr (DROP)
-              drop_keep_masks(tk2, drop_fin(pre + (uint32_t)(16 * fi + r) * kDropC1, seed_kx(seed)), km[0], km[1]);
+          for (int r = 0; r < 4; r += 2) {  // keys r, r + 1: packed FMA / product pairs
+            uint32_t km[2][2] = {{~0u, ~0u}, {~0u, ~0u}};
+            if constexpr (DROP) {
+#pragma unroll
+              for (int e = 0; e < 2; ++e)
+                drop_keep_masks(tk2, drop_fin(pre + (uint32_t)(16 * fi + r + e) * kDropC1, seed_kx(seed)), km[e][0],
+                                km[e][1]);
+            }
 #pragma unroll
             for (int qg = 0; qg < 2; ++qg) {
-              float p = __builtin_amdgcn_exp2f(fmaf(s[qg][f][r], sl2, -lse2[qg]));
-              if constexpr (DIAG) p = (k_lo + 16 * fi + 4 * g + r > q_lo + 16 * qg + (lane & 15)) ? 0.f : p;
-              float d = dp[qg][f][r];
-              if constexpr (DROP) d = sel_mask(km[qg], d, -dl[qg]);
-              s[qg][f][r] = p * d;
+              f32x2 p = exp2_affine2(s[qg][f][r], s[qg][f][r + 1], sl2, -lse2[qg]);
+              f32x2 d = {dp[qg][f][r], dp[qg][f][r + 1]};
+#pragma unroll
+              for (int e = 0; e < 2; ++e) {
+                if constexpr (DIAG) p[e] = (k_lo + 16 * fi + 4 * g + r + e > q_lo + 16 * qg + (lane & 15)) ? 0.f : p[e];
+                if constexpr (DROP) d[e] = sel_mask(km[e][qg], d[e], -dl[qg]);
+              }
+              const f32x2 v = p * d;
+              s[qg][f][r] = v[0];
+              s[qg][f][r + 1] = v[1];
             }
           }
         }
@@ -587,8 +606,9 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkdv_kernel(const bf16* __res
   };
   auto sstore = [&](char* st) {
     if (threadIdx.x < BQ3) {
-      reinterpret_cast<float*>(st + 2 * kTile)[threadIdx.x] = rl * kLog2e;
-      reinterpret_cast<float*>(st + 2 * kTile + BQ3 * 4)[threadIdx.x] = rdl;
+      // both negated: the FMA addend and the dropped-key value of dP - delta as stored (no per-tile negations)
+      reinterpret_cast<float*>(st + 2 * kTile)[threadIdx.x] = -(rl * kLog2e);
+      reinterpret_cast<float*>(st + 2 * kTile + BQ3 * 4)[threadIdx.x] = -rdl;
     }
   };
   const int i0 = kb * 128 / BQ3;
@@ -609,13 +629,13 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkdv_kernel(const bf16* __res
       const bool diag = q0 < k_lo + 31;
       const uint32_t pre_t = DROP ? drop_pre(seed32(seed), ((uint32_t)bh * T + q0 + 4 * g) * (uint32_t)T + k_lo + (lane & 15)) : 0u;
       f32x4 s[2][2], dp[2][2];  // [kg][fl]: S[q = q0 + 16fl + 4g + r][key = k_lo + 16kg + (l&15)]
-      f32x4 l4[2], d4[2];
+      f32x4 nl4[2], nd4[2];  // -lse * log2(e), -delta of the tile's queries
 #pragma unroll
       for (int fl = 0; fl < 2; ++fl) {
-        l4[fl] = *reinterpret_cast<const f32x4*>(Ls + 16 * fl + 4 * g);
-        d4[fl] = *reinterpret_cast<const f32x4*>(Dl + 16 * fl + 4 * g);
+        nl4[fl] = *reinterpret_cast<const f32x4*>(Ls + 16 * fl + 4 * g);
+        nd4[fl] = *reinterpret_cast<const f32x4*>(Dl + 16 * fl + 4 * g);
         s[0][fl] = s[1][fl] = f32x4{0.f, 0.f, 0.f, 0.f};
-        dp[0][fl] = dp[1][fl] = -d4[fl];
+        dp[0][fl] = dp[1][fl] = nd4[fl];
       }
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
@@ -641,6 +661,16 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkdv_kernel(const bf16* __res
 #pragma unroll
         for (int kg = 0; kg < 2; ++kg) {
           const int key = k_lo + 16 * kg + (lane & 15);
+          // the scores' affine part in place, as packed FMA pairs (v_pk_fma_f32; no register beyond s): x = s * sl2 - lse
+#pragma unroll
+          for (int fl = 0; fl < 2; ++fl)
+#pragma unroll
+            for (int r = 0; r < 4; r += 2) {
+              const f32x2 t = __builtin_elementwise_fma(f32x2{s[kg][fl][r], s[kg][fl][r + 1]}, f32x2{sl2, sl2},
+                                                        f32x2{nl4[fl][r], nl4[fl][r + 1]});
+              s[kg][fl][r] = t[0];
+              s[kg][fl][r + 1] = t[1];
+            }
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             uint32_t km[2] = {~0u, ~0u};
@@ -652,12 +682,12 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkdv_kernel(const bf16* __res
             }
 #pragma unroll
             for (int fl = 0; fl < 2; ++fl) {
-              float p = __builtin_amdgcn_exp2f(fmaf(s[kg][fl][r], sl2, -l4[fl][r]));
+              float p = __builtin_amdgcn_exp2f(s[kg][fl][r]);
               if constexpr (DIAG) p = (q0 + 16 * fl + 4 * g + r < key) ? 0.f : p;
               float pdv = p, d = dp[kg][fl][r];
               if constexpr (DROP) {
                 pdv = __uint_as_float(km[fl] & __float_as_uint(p));
-                d = sel_mask(km[fl], d, -d4[fl][r]);
+                d = sel_mask(km[fl], d, nd4[fl][r]);
               }
               dp[kg][fl][r] = pdv;
               s[kg][fl][r] = p * d;
