@@ -76,7 +76,7 @@ def main():
     ap.add_argument("--model", default="124M")
     ap.add_argument("--dropout", type=float, default=0.1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--bucket-mb", type=float, default=25.0)
     # BASELINE configs 4-5 (350M / 1.5B under FSDP, 1.5B with gradient accumulation); a "step" is then one
     # optimizer step over grad_accum micro-batches of --batch sequences per rank
     ap.add_argument("--parallel", choices=["ddp", "fsdp"], default="ddp", help="multi-rank wrapper (N > 1)")
@@ -102,7 +102,8 @@ def main():
     if wrapped:
         from gpt_2_distributed_amd.parallel import DistributedDataParallel, ShardedDataParallel
         wrap = ShardedDataParallel if args.parallel == "fsdp" else DistributedDataParallel
-        ddp = wrap(model, bucket_mb=args.bucket_mb)
+        # DDP: the embedding bucket's all-reduce runs under the optimizer step of every other range
+        ddp = wrap(model, bucket_mb=args.bucket_mb, **({} if args.parallel == "fsdp" else {"overlap_optimizer": True}))
         opt = ddp.configure_optimizers(learning_rate=1e-4)
         fwd = ddp
     else:

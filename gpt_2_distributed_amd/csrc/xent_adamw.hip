@@ -313,15 +313,25 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g,
   if (threadIdx.x == 0) partials[blockIdx.x] = r[0] + r[1] + r[2] + r[3];
 }
 
-// Deterministic final reduction of per-block partials: out = sqrt(sum).
-__global__ __launch_bounds__(256) void norm_finalize_kernel(const float* __restrict__ partials, int n,
-                                                            float* __restrict__ out) {
+// Deterministic final reduction of per-block partials: out = sqrt(sum). One 1024-thread block whose threads load 4
+// partials per step before adding them (independent loads in flight: FSDP's per-unit optimizer hands it 14 x 2048
+// partials, 40 us with one dependent load per step at 256 threads)
+__global__ __launch_bounds__(1024) void norm_finalize_kernel(const float* __restrict__ partials, int n,
+                                                             float* __restrict__ out) {
   double s = 0.0;
-  for (int i = threadIdx.x; i < n; i += 256) s += partials[i];
-  __shared__ double r[256];
+  int i = threadIdx.x;
+  for (; i + 3 * 1024 < n; i += 4 * 1024) {
+    const float a = partials[i], b = partials[i + 1024], c = partials[i + 2048], d = partials[i + 3072];
+    s += a;
+    s += b;
+    s += c;
+    s += d;
+  }
+  for (; i < n; i += 1024) s += partials[i];
+  __shared__ double r[1024];
   r[threadIdx.x] = s;
   __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
+  for (int o = 512; o > 0; o >>= 1) {
     if (threadIdx.x < o) r[threadIdx.x] += r[threadIdx.x + o];
     __syncthreads();
   }
@@ -387,7 +397,7 @@ GPT2MI_EXPORT int gpt2mi_adamw(float* p, const float* g, float* m, float* v, uin
                                            grad_scale, partials);
   int rc = gpt2mi::check_launch("adamw");
   if (rc || !grad_norm) return rc;
-  norm_finalize_kernel<<<1, 256, 0, s>>>(partials, kNormBlocks, grad_norm);
+  norm_finalize_kernel<<<1, 1024, 0, s>>>(partials, kNormBlocks, grad_norm);
   return gpt2mi::check_launch("adamw_norm");
 }
 
@@ -397,7 +407,7 @@ GPT2MI_EXPORT int gpt2mi_grad_norm(const float* g, size_t n, float scale, float*
   sumsq_kernel<<<kNormBlocks, 256, 0, s>>>(g, n / 4, scale, partials);
   int rc = gpt2mi::check_launch("grad_norm");
   if (rc) return rc;
-  norm_finalize_kernel<<<1, 256, 0, s>>>(partials, kNormBlocks, out);
+  norm_finalize_kernel<<<1, 1024, 0, s>>>(partials, kNormBlocks, out);
   return gpt2mi::check_launch("grad_norm_finalize");
 }
 
@@ -405,7 +415,7 @@ GPT2MI_EXPORT int gpt2mi_norm_partials_size(void) { return kNormBlocks; }
 
 GPT2MI_EXPORT int gpt2mi_norm_finalize(const float* partials, int n, float* out, void* stream) {
   GPT2MI_REQUIRE(n > 0, "norm_finalize: n=%d", n);
-  norm_finalize_kernel<<<1, 256, 0, (hipStream_t)stream>>>(partials, n, out);
+  norm_finalize_kernel<<<1, 1024, 0, (hipStream_t)stream>>>(partials, n, out);
   return gpt2mi::check_launch("norm_finalize");
 }
 

@@ -64,6 +64,13 @@ class FusedAdamW(_FlatAdamW):
         super().__init__(list(model.parameters()), model.arena, lr, betas, eps, weight_decay)
         self.model = model
         self.engine = model.engine()
+        self.tail_source = None
+
+    def attach_tail(self, hooks):
+        """DistributedDataParallel(overlap_optimizer=True): ``hooks.take_tail()`` hands over the backward's last bucket
+        (work, lo, hi) still in flight; step() updates the arena outside [lo, hi) first, then waits for it."""
+        self.tail_source = hooks
+        self.partials = torch.empty(3 * K.norm_partials_size(), dtype=torch.float32, device=self.partials.device)
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -73,9 +80,30 @@ class FusedAdamW(_FlatAdamW):
                 loss = closure()
         eng = self.engine
         if all(p.grad is None for p in eng.params_by_name.values()):
+            if self.tail_source is not None:
+                self.tail_source.wait_tail()
             return loss  # no gradients since zero_grad(set_to_none=True): torch's optimizers skip such params
         self.step_count += 1
-        self._run(self.model.arena, eng.grad, eng.shadow)
+        tail = self.tail_source.take_tail() if self.tail_source is not None else None
+        arena, n = self.model.arena, self.model.arena.numel()
+        if tail is not None and (tail[1] % 4 or tail[2] % 4):  # the kernel takes 4-element groups
+            tail[0].wait()
+            tail = None
+        if tail is None:
+            self._run(arena, eng.grad, eng.shadow)
+        else:
+            # the ranges outside the in-flight bucket run under its all-reduce; then the bucket's own range. The
+            # grad-norm partial sums of the pieces go to one buffer, finalised once (the same per-element updates and
+            # the same norm as one launch: tests/test_kernels_gpu.py::test_adamw_in_pieces_with_one_norm_finalisation)
+            work, lo, hi = tail
+            P, k = K.norm_partials_size(), 0
+            for a, b in ((0, lo), (hi, n)):
+                if b > a:
+                    self._run(arena, eng.grad, eng.shadow[a:b], a, b, self.partials[k * P:(k + 1) * P])
+                    k += 1
+            work.wait()
+            self._run(arena, eng.grad, eng.shadow[lo:hi], lo, hi, self.partials[k * P:(k + 1) * P])
+            K.norm_finalize(self.partials, (k + 1) * P, self.grad_norm)
         eng.mark_shadow_fresh()
         return loss
 
@@ -83,6 +111,8 @@ class FusedAdamW(_FlatAdamW):
         # The grads are views of one arena. set_to_none (torch's default): unbind them; the next backward
         # rebinds, and a whole-model backward then zeroes only the accumulated slots (its weight-gradient
         # GEMMs write theirs). Otherwise zero the arena in one memset and keep the views bound.
+        if self.tail_source is not None:
+            self.tail_source.wait_tail()  # a deferred bucket still writes its range of the arena
         if set_to_none:
             for p in self.engine.params_by_name.values():
                 p.grad = None

@@ -122,6 +122,7 @@ class BucketedReducer:
         self.pending_lo = None  # unsent contiguous span [lo, hi)
         self.pending_hi = None
         self.works = []
+        self.spans = []         # [lo, hi) of each issued bucket
         self.launched = 0       # buckets issued during the backward (before finish)
 
     def mark_ready(self, name: str):
@@ -148,18 +149,25 @@ class BucketedReducer:
             return
         span = self.flat[self.pending_lo:self.pending_hi]
         self.works.append(dist.all_reduce(span, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+        self.spans.append((self.pending_lo, self.pending_hi))
         self.launched += 1
         self.pending_lo = self.pending_hi = None
 
-    def finish(self):
+    def finish(self, defer_last: bool = False):
         """Issue whatever is left, then make the current stream wait on every bucket (nccl: a stream
-        wait, the host does not block; gloo: the host waits)."""
+        wait, the host does not block; gloo: the host waits). defer_last: the last bucket (the embeddings, final only
+        at the end of the backward) is left in flight and returned as (work, lo, hi) for the caller to wait on."""
         if self.next < len(self.order):
             self.mark_ready(self.order[-1][0])
         self._launch()
-        for w in self.works:
+        works, tail = self.works, None
+        if defer_last and works:
+            tail = (works[-1],) + self.spans[-1]
+            works = works[:-1]
+        for w in works:
             w.wait()
         self.reset()
+        return tail
 
 
 class _DPHooks(GradHooks):
@@ -184,8 +192,23 @@ class _DDPHooks(_DPHooks):
     def __init__(self, engine, world, reducer):
         super().__init__(engine, world)
         self.reducer = reducer
+        # DistributedDataParallel(overlap_optimizer=True) with the fused AdamW: the backward returns with its last bucket
+        # (work, lo, hi) still in flight, and the optimizer updates every other range under it (optim.FusedAdamW.step)
+        self.defer_tail = False
+        self.tail = None
+
+    def take_tail(self):
+        t, self.tail = self.tail, None
+        return t
+
+    def wait_tail(self):
+        """Make the current stream wait for a deferred last bucket (its gradients final from here on)."""
+        t = self.take_tail()
+        if t is not None:
+            t[0].wait()
 
     def begin_backward(self) -> float:
+        self.wait_tail()  # the next backward writes the deferred range again
         if self.sync and self.coll:
             # a backward that raised midway left buckets in flight and `next` past them: wait for those (their
             # spans are re-reduced by this backward anyway) and start over
@@ -198,7 +221,8 @@ class _DDPHooks(_DPHooks):
         # from the first bucket on, RCCL runs under the rest of the backward (no persistent GEMM grid there); the
         # lm_head backward and the last blocks' backward before the first full bucket keep the persistent schedule
         # (a host-side event query: a bucket that reads complete is certainly done before anything enqueued now runs)
-        return self.sync and self.coll and any(not w.is_completed() for w in self.reducer.works)
+        return (self.sync and self.coll and any(not w.is_completed() for w in self.reducer.works)) or \
+            (self.tail is not None and not self.tail[0].is_completed())
 
     def ready(self, name):
         if self.sync and self.coll:
@@ -206,15 +230,25 @@ class _DDPHooks(_DPHooks):
 
     def end_backward(self):
         if self.sync and self.coll:
-            self.reducer.finish()
+            self.tail = self.reducer.finish(defer_last=self.defer_tail)
 
 
 class DistributedDataParallel(nn.Module):
-    """DDP for the arena model: same call surface as torch DDP for the reference loop."""
+    """DDP for the arena model: same call surface as torch DDP for the reference loop.
 
-    def __init__(self, module, device_ids=None, bucket_mb: float = 64.0, broadcast: bool = True):
+    ``bucket_mb`` defaults to torch DDP's ``bucket_cap_mb`` (25, the reference's DDP(model) at
+    train_gpt2_distributed.py:163): at the GPT-2 widths every GPT2Block (28 MB fp32 at 124M) is its own bucket, so
+    only the block-0 and embedding buckets follow the last backward kernels. ``overlap_optimizer=True`` (bench.py,
+    the trainer): with this wrapper's ``configure_optimizers`` AdamW, the backward returns with the embedding bucket
+    still in flight and the optimizer step updates every other range under it — the embedding gradients are then
+    final only after ``optimizer.step()`` or ``finish_gradient_sync()`` (torch DDP semantics, the default, make them
+    final when ``loss.backward()`` returns)."""
+
+    def __init__(self, module, device_ids=None, bucket_mb: float = 25.0, broadcast: bool = True,
+                 overlap_optimizer: bool = False):
         super().__init__()
         self.module = module
+        self.overlap_optimizer = overlap_optimizer
         eng = module.engine()
         self.engine = eng
         world = dist.get_world_size()
@@ -239,10 +273,18 @@ class DistributedDataParallel(nn.Module):
         return self.module(*args, **kwargs)
 
     def finish_gradient_sync(self):
-        """Kept for callers of round 1: the backward itself completes the gradient collective."""
+        """Make the gradients final on the current stream: a no-op unless overlap_optimizer left the last bucket in
+        flight (the backward itself completes every other bucket)."""
+        self.hooks.wait_tail()
 
     def configure_optimizers(self, *a, **kw):
-        return self.module.configure_optimizers(*a, **kw)
+        opt = self.module.configure_optimizers(*a, **kw)
+        if self.overlap_optimizer:
+            from .optim import FusedAdamW
+            if isinstance(opt, FusedAdamW):  # the only optimizer that waits for a deferred bucket itself
+                opt.attach_tail(self.hooks)
+                self.hooks.defer_tail = True
+        return opt
 
     def state_dict(self, *a, **kw):
         return self.module.state_dict(*a, **kw)

@@ -178,7 +178,7 @@ def main(argv=None):
     config = dataclasses.replace(GPT2Config(), n_positions=args.seq_len, **over)
     base = GPT2(config).to(device)
     if args.training_mode == "ddp":
-        model = DistributedDataParallel(base)
+        model = DistributedDataParallel(base, overlap_optimizer=True)  # the grad norm comes from the fused AdamW
     elif args.training_mode == "fsdp":
         model = FullyShardedDataParallel(base)
     else:

@@ -12,6 +12,8 @@ Variants (one torch.distributed.run launch runs them all):
   ddp/torch     torch.optim.AdamW(fused) + torch clip_grad_norm_ on the wrapper's parameters: the
                 gradients must be final when loss.backward() returns
   ddp/nosync    no_sync() on the non-final micro-step (the repo trainer's choice; same math)
+  ddp/overlap   the fused AdamW with overlap_optimizer=True: the last bucket stays in flight after the backward and
+                the optimizer updates every other range under it (bench.py / the trainer)
   fsdp/fused    per-GPT2Block FULL_SHARD units, per-unit bf16/fp32 all-gather + reduce-scatter
   fsdp/torch    torch.optim.AdamW on the FSDP flat shard, whose zero_grad(set_to_none=True) drops flat_param.grad:
                 the next backward must overwrite the grad shard, not add to the stale one
@@ -25,7 +27,8 @@ concatenated batch, Zipf tokens stored in the file):
   cfg4_golden.json    BASELINE cfg 4's widths (GPT-2 350M: C=1024, H=16, V=50257) on 2 layers, T=1024, B=1 per rank,
                       grad_accum=2, through FullyShardedDataParallel (2 gloo ranks, and 1 forced-RCCL rank);
   ddp124_golden.json  cfg 3's widths (GPT-2 124M: C=768, H=12, V=50257, T=1024) on 2 layers, B=2 per rank, through
-                      DistributedDataParallel with its default 64 MiB buckets.
+                      DistributedDataParallel with its default 25 MiB buckets (torch DDP's bucket_cap_mb), also with
+                      overlap_optimizer (the embedding bucket in flight under the optimizer step).
 """
 import json
 import os
@@ -58,9 +61,10 @@ else:
     toks = torch.randint(0, 509, (S, GA, w * P, 65), generator=torch.Generator().manual_seed(5))
 BUCKET_MB = float(os.environ.get("BUCKET_MB", "0.25"))
 
-def build(mode, opt_kind):
+def build(mode, opt_kind, overlap=False):
     m = GPT2(cfg).to("cuda:0")
-    wrap = FullyShardedDataParallel(m) if mode == "fsdp" else DistributedDataParallel(m, bucket_mb=BUCKET_MB)
+    wrap = FullyShardedDataParallel(m) if mode == "fsdp" else DistributedDataParallel(m, bucket_mb=BUCKET_MB,
+                                                                                      overlap_optimizer=overlap)
     if opt_kind == "torch":
         opt = torch.optim.AdamW(wrap.parameters(), lr=G["lr"], weight_decay=0.1, betas=(0.9, 0.95), fused=True)
     else:
@@ -99,7 +103,7 @@ res = {}
 for variant in os.environ["VARIANTS"].split(","):
     mode, kind, prec = variant.split("/")
     opt_kind = "torch" if kind == "torch" else "fused"
-    m, wrap, opt = build(mode, opt_kind)
+    m, wrap, opt = build(mode, opt_kind, overlap=kind == "overlap")
     losses, norms = [], []
     if kind == "ckpt":
         step(wrap, opt, 0, prec, opt_kind, False)
@@ -124,7 +128,7 @@ if r == 0:
 dist.barrier(); dist.destroy_process_group()
 """
 
-VARIANTS = ["ddp/fused/fp32", "ddp/fused/bf16", "ddp/torch/fp32", "ddp/nosync/fp32", "fsdp/fused/fp32",
+VARIANTS = ["ddp/fused/fp32", "ddp/fused/bf16", "ddp/overlap/fp32", "ddp/torch/fp32", "ddp/nosync/fp32", "fsdp/fused/fp32",
             "fsdp/fused/bf16", "fsdp/torch/fp32", "fsdp/ckpt/bf16", "ddp/ckpt/fp32"]
 
 
@@ -148,7 +152,8 @@ def results(tmp_path_factory):
                    GPT2MI_DIST_BACKEND="gloo")
 
 
-RCCL_VARIANTS = ["ddp/fused/fp32", "ddp/fused/bf16", "ddp/torch/fp32", "fsdp/fused/fp32", "fsdp/fused/bf16"]
+RCCL_VARIANTS = ["ddp/fused/fp32", "ddp/fused/bf16", "ddp/overlap/bf16", "ddp/torch/fp32", "fsdp/fused/fp32",
+                 "fsdp/fused/bf16"]
 
 
 @pytest.fixture(scope="module")
@@ -208,9 +213,9 @@ WIDE_RUNS = {  # (golden file, ranks, backend, variants, extra env)
     "cfg5_rccl1": ("cfg5_golden.json", 1, "nccl", ["fsdp/fused/fp32", "fsdp/fused/bf16"], {}),
     "cfg4_gloo2": ("cfg4_golden.json", 2, "gloo", ["fsdp/fused/fp32", "fsdp/fused/bf16", "fsdp/torch/fp32"], {}),
     "cfg4_rccl1": ("cfg4_golden.json", 1, "nccl", ["fsdp/fused/fp32", "fsdp/fused/bf16"], {}),
-    "ddp124_gloo2": ("ddp124_golden.json", 2, "gloo", ["ddp/fused/fp32", "ddp/fused/bf16", "ddp/torch/fp32"],
-                     {"BUCKET_MB": "64"}),
-    "ddp124_rccl1": ("ddp124_golden.json", 1, "nccl", ["ddp/fused/bf16"], {"BUCKET_MB": "64"}),
+    "ddp124_gloo2": ("ddp124_golden.json", 2, "gloo", ["ddp/fused/fp32", "ddp/fused/bf16", "ddp/overlap/bf16",
+                                                        "ddp/torch/fp32"], {"BUCKET_MB": "25"}),
+    "ddp124_rccl1": ("ddp124_golden.json", 1, "nccl", ["ddp/fused/bf16", "ddp/overlap/bf16"], {"BUCKET_MB": "25"}),
 }
 
 
@@ -232,7 +237,7 @@ def wide_results(tmp_path_factory):
 @pytest.mark.parametrize("run,variant", [(r, v) for r, spec in WIDE_RUNS.items() for v in spec[3]])
 def test_production_width_vs_reference(wide_results, run, variant):
     """BASELINE cfg 5 (1.5B widths, FSDP, grad_accum 2), cfg 4 (350M widths, FSDP FULL_SHARD, grad_accum 2) and cfg 3
-    (124M widths, DDP, 64 MiB buckets) through the wrappers against the reference on the concatenated batch: loss,
+    (124M widths, DDP, 25 MiB buckets) through the wrappers against the reference on the concatenated batch: loss,
     grad norm and final parameters, fp32 within 1e-4 and bf16 autocast within 2e-2."""
     gold, nproc = WIDE_RUNS[run][0], WIDE_RUNS[run][1]
     _check_vs_golden(wide_results[run][variant], variant, GOLD=WIDE[gold], world=nproc)

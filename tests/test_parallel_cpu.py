@@ -63,6 +63,32 @@ def _bucketed(rank, world):
     return (torch.allclose(flat, expect, atol=1e-6), n_launched, red.launched == 0 and red.next == 0)
 
 
+def _bucketed_deferred(rank, world):
+    """finish(defer_last=True) (DistributedDataParallel(overlap_optimizer=True)): every bucket but the last is complete
+    when finish returns; the last is handed back as (work, lo, hi) over the range that became final last."""
+    from gpt_2_distributed_amd.parallel import BucketedReducer
+    n = 10_000
+    flat = torch.randn(n, generator=torch.Generator().manual_seed(rank)) / world
+    expect = sum(torch.randn(n, generator=torch.Generator().manual_seed(r)) for r in range(world)) / world
+    bounds = [0, 1000, 2500, 4000, 7000, 9000, n]
+    order = [(f"r{i}", bounds[i], bounds[i + 1]) for i in reversed(range(len(bounds) - 1))]
+    red = BucketedReducer(flat, order, bucket_mb=2000 * 4 / 2**20)
+    for name, _, _ in order[:-1]:
+        red.mark_ready(name)
+    work, lo, hi = red.finish(defer_last=True)
+    work.wait()
+    return (torch.allclose(flat, expect, atol=1e-6), lo, hi, red.launched == 0 and red.next == 0)
+
+
+def test_bucketed_allreduce_deferred_last_bucket_gloo():
+    out = _spawn(_bucketed_deferred)
+    for r, v in out.items():
+        assert isinstance(v, tuple), v
+        ok, lo, hi, was_reset = v
+        assert ok and was_reset
+        assert (lo, hi) == (0, 1000)  # the embeddings' range (first in the arena, final last)
+
+
 def test_bucketed_allreduce_gloo():
     out = _spawn(_bucketed)
     for r, v in out.items():
