@@ -210,7 +210,24 @@ __global__ __launch_bounds__(1024) void xent_finalize_kernel(const float* __rest
                                                             const int64_t* __restrict__ labels, int M, int ignore_index,
                                                             float* __restrict__ loss, float* __restrict__ inv_count) {
   float s = 0.f, n = 0.f;
-  for (int i = threadIdx.x; i < M; i += 1024) {
+  // four rows' loads issued together, then added in row order (the same sums as one row per step: 33 us with one
+  // dependent load at a time over cfg 2's 65536 rows)
+  int i = threadIdx.x;
+  for (; i + 3 * 1024 < M; i += 4 * 1024) {
+    float l[4];
+    int64_t y[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      l[k] = loss_rows[i + 1024 * k];
+      y[k] = labels[i + 1024 * k];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      s += l[k];
+      n += (y[k] == ignore_index) ? 0.f : 1.f;
+    }
+  }
+  for (; i < M; i += 1024) {
     s += loss_rows[i];
     n += (labels[i] == ignore_index) ? 0.f : 1.f;
   }
