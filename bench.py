@@ -15,6 +15,10 @@ Also reported:
   roofline     for the dominant kernel (the tied lm_head GEMMs are the largest launches): algorithmic
                FLOP per launch / average launch time measured live with HIP events on the launch stream
   kernels      the same for every probed launch family
+Probed launches: every launch of the probed families in every --probe-every'th timed step (default 5: steps 0, 5, 10,
+15 of the default 20), so each launch of a step is sampled equally often. Each probed launch costs two event
+records inside the timed region: probing all ≈ 76 launches of every step (rounds 1-4) cost 58.68 vs 58.49 ms per step
+at every 5th step and 58.42 with the first step alone (profiles/r4pr/, same box, alternating runs).
   cpu_baseline the oracle (CPU restatement of the reference step, oracle/train_ref.py) timed on this
                host's cores on a bounded sample (rank 0, N = 1 only)
 """
@@ -81,6 +85,8 @@ def main():
     # optimizer step over grad_accum micro-batches of --batch sequences per rank
     ap.add_argument("--parallel", choices=["ddp", "fsdp"], default="ddp", help="multi-rank wrapper (N > 1)")
     ap.add_argument("--grad_accum", type=int, default=1)
+    ap.add_argument("--probe-every", type=int, default=5,
+                    help="time the probed kernel launches (HIP events) in every N-th timed step")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -139,18 +145,20 @@ def main():
     if wrapped:
         dist.barrier()
     probes = ["lm_head_fwd", "lm_head_dgrad", "lm_head_wgrad", "fc1_fwd", "attn_fwd", "wgrad"]
-    eng.probes = {p: [] for p in probes}
+    armed = {p: [] for p in probes}
+    every = max(1, args.probe_every)
     torch.cuda.synchronize()
     if wrapped:
         dist.barrier()
     t0 = time.perf_counter()
     for i in range(args.steps):
+        eng.probes = armed if i % every == 0 else {}  # the sampled steps record events around every probed launch
         loss = step(i)
     torch.cuda.synchronize()
     if wrapped:
         dist.barrier()
     dt = time.perf_counter() - t0
-    eng.probes, armed = {}, eng.probes
+    eng.probes = {}
     dt_t = torch.tensor([dt], device=dev)
     if wrapped:
         dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
