@@ -341,12 +341,15 @@ class _FSDPHooks(_DPHooks):
         f = self.fsdp
         if not f.coll:
             return False
-        return any(w is not None and not w.is_completed() for w, _ in f._pending.values()) or \
+        return any(w is not None and u not in f._fenced and not w.is_completed() for u, (w, _) in f._pending.items()) or \
             any(w is not None and not w.is_completed() for _, w, _ in f._rs_works)
 
 
 class FullyShardedDataParallel(nn.Module):
     """FULL_SHARD data parallelism over per-GPT2Block units (see the module docstring)."""
+
+    # the forward unit (index in arena order: embed, h.0, h.1, h.2, ...) at which every pending all-gather is waited for
+    FENCE_UNIT = 3
 
     def __init__(self, module, device_ids=None, bucket_mb: float = 64.0, prefetch: bool = True,
                  prefetch_depth: Optional[int] = None):
@@ -381,6 +384,9 @@ class FullyShardedDataParallel(nn.Module):
         self._bufs: Dict[tuple, torch.Tensor] = {}
         self._valid: Dict[str, Optional[torch.dtype]] = {u: None for u in self.order}
         self._pending: Dict[str, tuple] = {}       # unit -> (work, dtype) of an in-flight all-gather
+        # pending all-gathers the compute stream already waits for (fenced at unit FENCE_UNIT of the forward): no kernel
+        # enqueued after the fence can overlap them, so they do not count as in flight for the GEMM schedule
+        self._fenced = set()
         self._rs_works: List[tuple] = []            # (unit, work, out) of in-flight reduce-scatters
         # every unit's bf16_chunk == bf16(its flat_param range) (set by our AdamW, which writes them)
         self._bf16_fresh = False
@@ -465,6 +471,7 @@ class FullyShardedDataParallel(nn.Module):
         else:
             work = dist.all_gather_into_tensor(out, src, async_op=True)
         self._pending[unit] = (work, dtype)
+        self._fenced.discard(unit)  # a new gather of the unit: not waited for yet
 
     def _gather_for(self, unit):
         from . import _lib as K
@@ -480,11 +487,20 @@ class FullyShardedDataParallel(nn.Module):
             for nxt in self.order[i + 1:last]:
                 if self._valid.get(nxt) != dtype and nxt not in self._pending:
                     self._issue_gather(nxt, dtype)
+        if self.coll and self.order.index(unit) >= min(self.FENCE_UNIT, len(self.order) - 1):
+            # every gather still pending is waited for here (a stream wait): they were issued at the first unit and are
+            # done by now at any world size, so this costs nothing, and the rest of the forward's GEMMs keep the static
+            # persistent schedule (GradHooks.inflight) instead of the work-queue variant
+            for u, (w, _) in self._pending.items():
+                if w is not None and u not in self._fenced:
+                    w.wait()
+                    self._fenced.add(u)
         if self._valid.get(unit) == dtype:
             return
         work, _ = self._pending.pop(unit)
-        if work is not None:
+        if work is not None and unit not in self._fenced:
             work.wait()
+        self._fenced.discard(unit)
         p = self.plan[unit]
         out = self._buf("ag", unit, dtype, p.per * self.world)
         bf = eng.shadow[p.lo:p.hi] if dtype == torch.bfloat16 else None
