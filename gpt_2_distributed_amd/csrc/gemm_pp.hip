@@ -301,11 +301,6 @@ __device__ __forceinline__ void xcd_range(int x, int n, int& base, int& cnt) {
 }
 
 // Output tile of item `pid` (GM M-tiles per group share their B tiles in L2).
-// GEMM_SLAB_TEMPORAL (A/B): the split-K fp32 slabs written with default-policy stores instead of non-temporal ones
-#ifndef GEMM_SLAB_TEMPORAL
-#define GEMM_SLAB_TEMPORAL 0
-#endif
-GPT2MI_PRODUCT_KNOB(GEMM_SLAB_TEMPORAL, 0);
 #ifndef GPT2MI_PP_GM
 #define GPT2MI_PP_GM 4
 #endif
@@ -904,8 +899,11 @@ write_image(mi, wr * 64);
       v += bias;
       if constexpr (EPI == EPI_SLAB) {
         float* slab = reinterpret_cast<float*>(P.C) + (size_t)split * P.M * P.ldc;
-        if constexpr (GEMM_SLAB_TEMPORAL) *reinterpret_cast<f32x4*>(slab + (size_t)gm * P.ldc + gn) = v;
-        else store4<float>(slab + (size_t)gm * P.ldc + gn, v);
+        // default-policy stores, not the non-temporal ones of the other epilogues: the split-K reduction reads the
+        // slabs right after this launch (same-process A/B, same bits: qkv / proj / fc2 wgrad + reduction 1-3.5 %
+        // faster, fc1 within noise; profiles/r4fin/slab_store_ab.log)
+        if constexpr (GEMM_STORE_EXP == 1) asm volatile("" ::"v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]));
+        else *reinterpret_cast<f32x4*>(slab + (size_t)gm * P.ldc + gn) = v;
       } else if constexpr (EPI == EPI_SLAB16) {  // 8 B per lane: one 512-B bf16 row per wave-instruction
         bf16* slab = reinterpret_cast<bf16*>(P.C) + (size_t)split * P.M * P.ldc;
         store4<bf16>(slab + (size_t)gm * P.ldc + gn, v);
