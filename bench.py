@@ -108,8 +108,8 @@ def main():
     if wrapped:
         from gpt_2_distributed_amd.parallel import DistributedDataParallel, ShardedDataParallel
         wrap = ShardedDataParallel if args.parallel == "fsdp" else DistributedDataParallel
-        # DDP: the embedding bucket's all-reduce runs under the optimizer step of every other range
-        ddp = wrap(model, bucket_mb=args.bucket_mb, **({} if args.parallel == "fsdp" else {"overlap_optimizer": True}))
+        # the embeddings' all-reduce (DDP) / reduce-scatter (FSDP) runs under the optimizer step of every other range
+        ddp = wrap(model, bucket_mb=args.bucket_mb, overlap_optimizer=True)
         opt = ddp.configure_optimizers(learning_rate=1e-4)
         fwd = ddp
     else:

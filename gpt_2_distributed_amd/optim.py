@@ -140,11 +140,20 @@ class ShardedAdamW(_FlatAdamW):
                 loss = closure()
         f = self.fsdp
         if f.flat_param.grad is None:
+            f.wait_tail()
             return loss  # no backward since zero_grad(set_to_none=True): skipped, as torch's optimizers do
         self.step_count += 1
         p = f.flat_param.detach()
         P = K.norm_partials_size()
-        for i, q in enumerate(f.plans):
+        # a unit whose reduce-scatter is still in flight (FullyShardedDataParallel(overlap_optimizer=True)) goes last,
+        # after every other unit's update has been enqueued under it
+        tail = f.tail_unit()
+        order = [i for i, q in enumerate(f.plans) if q.name != tail] + \
+            [i for i, q in enumerate(f.plans) if q.name == tail]
+        for i in order:
+            q = f.plans[i]
+            if q.name == tail:
+                f.wait_tail()
             self._run(p, f.grad_shard, f.bf16_chunk(q.name), q.soff, q.soff + q.per, self.unit_partials[i * P:(i + 1) * P])
         f.mark_params_updated(bf16_fresh=True)
         # the clip_grad_norm_(inf) value of the full model: sum of squares over units (one finalisation) and shards

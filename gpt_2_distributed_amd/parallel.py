@@ -323,6 +323,10 @@ class _FSDPHooks(_DPHooks):
         super().__init__(fsdp.engine, world)
         self.fsdp = fsdp
 
+    def begin_backward(self) -> float:
+        self.fsdp.wait_tail()  # the next backward packs and reduce-scatters the deferred unit again
+        return super().begin_backward()
+
     def ready(self, name):
         if self.sync:
             self.fsdp._reduce_scatter(name)
@@ -342,7 +346,8 @@ class _FSDPHooks(_DPHooks):
         if not f.coll:
             return False
         return any(w is not None and u not in f._fenced and not w.is_completed() for u, (w, _) in f._pending.items()) or \
-            any(w is not None and not w.is_completed() for _, w, _ in f._rs_works)
+            any(w is not None and not w.is_completed() for _, w, _ in f._rs_works) or \
+            (f._tail is not None and f._tail[1] is not None and not f._tail[1].is_completed())
 
 
 class FullyShardedDataParallel(nn.Module):
@@ -352,9 +357,16 @@ class FullyShardedDataParallel(nn.Module):
     FENCE_UNIT = 3
 
     def __init__(self, module, device_ids=None, bucket_mb: float = 64.0, prefetch: bool = True,
-                 prefetch_depth: Optional[int] = None):
+                 prefetch_depth: Optional[int] = None, overlap_optimizer: bool = False):
         super().__init__()
         self.module = module
+        # overlap_optimizer (with configure_optimizers' ShardedAdamW): the backward returns with the last unit's
+        # reduce-scatter (the embeddings, final only after the embedding backward) in flight, and the optimizer updates
+        # every other unit under it; flat_param.grad of that unit is final after optimizer.step() or
+        # finish_gradient_sync() (by default it is final when loss.backward() returns)
+        self.overlap_optimizer = overlap_optimizer
+        self._defer_tail = False
+        self._tail = None  # (unit, work, out, accumulate) of the deferred reduce-scatter
         eng = module.engine()
         self.engine = eng
         self.world = dist.get_world_size()
@@ -538,13 +550,33 @@ class FullyShardedDataParallel(nn.Module):
         # accumulate only into a gradient the caller still holds: after a torch optimizer's
         # zero_grad(set_to_none=True) flat_param.grad is None and the shard's old values are stale
         acc = self.flat_param.grad is self.grad_shard
-        for u, work, out in self._rs_works:
+        works = self._rs_works
+        if self._defer_tail and self.coll and works:
+            u, work, out = works[-1]
+            self._tail = (u, work, out, acc)
+            works = works[:-1]
+        for u, work, out in works:
             if work is not None:
                 work.wait()
             p = self.plan[u]
             K.fsdp_accum(out, self.grad_shard[p.soff:p.soff + p.per], p.per, accumulate=acc)
         self._rs_works = []
         self.flat_param.grad = self.grad_shard
+
+    def tail_unit(self) -> Optional[str]:
+        """The unit whose reduce-scatter overlap_optimizer left in flight (None if none)."""
+        return self._tail[0] if self._tail is not None else None
+
+    def wait_tail(self):
+        """Complete a deferred reduce-scatter: the current stream waits for it and accumulates its shard."""
+        from . import _lib as K
+        t, self._tail = self._tail, None
+        if t is not None:
+            u, work, out, acc = t
+            if work is not None:
+                work.wait()
+            p = self.plan[u]
+            K.fsdp_accum(out, self.grad_shard[p.soff:p.soff + p.per], p.per, accumulate=acc)
 
     @contextlib.contextmanager
     def no_sync(self):
@@ -559,10 +591,13 @@ class FullyShardedDataParallel(nn.Module):
         return self.module(*args, **kwargs)
 
     def finish_gradient_sync(self):
-        """Kept for callers of round 1: the backward itself completes the gradient collective."""
+        """Make the gradient shard final on the current stream: a no-op unless overlap_optimizer left the last unit's
+        reduce-scatter in flight (the backward itself completes every other one)."""
+        self.wait_tail()
 
     def zero_grad(self, set_to_none: bool = True):
         from . import _lib as K
+        self.wait_tail()  # its accumulate writes the shard; its reduce-scatter the unit's packing buffer
         if set_to_none:  # the next backward writes the shard instead of adding to it (_finish_reduce)
             self.flat_param.grad = None
         else:
@@ -573,6 +608,7 @@ class FullyShardedDataParallel(nn.Module):
     def configure_optimizers(self, weight_decay=0.1, learning_rate=1e-4, betas=(0.9, 0.95), device_type=None,
                              eps=1e-8):
         from .optim import ShardedAdamW
+        self._defer_tail = self.overlap_optimizer  # ShardedAdamW.step waits for the deferred unit itself
         return ShardedAdamW(self, lr=learning_rate, betas=betas, eps=eps, weight_decay=weight_decay)
 
     # ---- full state (checkpointing): collective, every rank calls --------------------------------------

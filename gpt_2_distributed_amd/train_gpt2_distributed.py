@@ -180,7 +180,7 @@ def main(argv=None):
     if args.training_mode == "ddp":
         model = DistributedDataParallel(base, overlap_optimizer=True)  # the grad norm comes from the fused AdamW
     elif args.training_mode == "fsdp":
-        model = FullyShardedDataParallel(base)
+        model = FullyShardedDataParallel(base, overlap_optimizer=True)
     else:
         model = base
     optim = model.configure_optimizers(weight_decay=0.1, learning_rate=args.lr, betas=(0.9, 0.95))

@@ -14,6 +14,7 @@ Variants (one torch.distributed.run launch runs them all):
   ddp/nosync    no_sync() on the non-final micro-step (the repo trainer's choice; same math)
   ddp/overlap   the fused AdamW with overlap_optimizer=True: the last bucket stays in flight after the backward and
                 the optimizer updates every other range under it (bench.py / the trainer)
+  fsdp/overlap  the same for FSDP: the last unit's reduce-scatter in flight under the other units' AdamW
   fsdp/fused    per-GPT2Block FULL_SHARD units, per-unit bf16/fp32 all-gather + reduce-scatter
   fsdp/torch    torch.optim.AdamW on the FSDP flat shard, whose zero_grad(set_to_none=True) drops flat_param.grad:
                 the next backward must overwrite the grad shard, not add to the stale one
@@ -63,8 +64,8 @@ BUCKET_MB = float(os.environ.get("BUCKET_MB", "0.25"))
 
 def build(mode, opt_kind, overlap=False):
     m = GPT2(cfg).to("cuda:0")
-    wrap = FullyShardedDataParallel(m) if mode == "fsdp" else DistributedDataParallel(m, bucket_mb=BUCKET_MB,
-                                                                                      overlap_optimizer=overlap)
+    wrap = FullyShardedDataParallel(m, overlap_optimizer=overlap) if mode == "fsdp" else \
+        DistributedDataParallel(m, bucket_mb=BUCKET_MB, overlap_optimizer=overlap)
     if opt_kind == "torch":
         opt = torch.optim.AdamW(wrap.parameters(), lr=G["lr"], weight_decay=0.1, betas=(0.9, 0.95), fused=True)
     else:
@@ -128,7 +129,8 @@ if r == 0:
 dist.barrier(); dist.destroy_process_group()
 """
 
-VARIANTS = ["ddp/fused/fp32", "ddp/fused/bf16", "ddp/overlap/fp32", "ddp/torch/fp32", "ddp/nosync/fp32", "fsdp/fused/fp32",
+VARIANTS = ["ddp/fused/fp32", "ddp/fused/bf16", "ddp/overlap/fp32", "ddp/torch/fp32", "ddp/nosync/fp32",
+            "fsdp/overlap/fp32", "fsdp/fused/fp32",
             "fsdp/fused/bf16", "fsdp/torch/fp32", "fsdp/ckpt/bf16", "ddp/ckpt/fp32"]
 
 
@@ -153,7 +155,7 @@ def results(tmp_path_factory):
 
 
 RCCL_VARIANTS = ["ddp/fused/fp32", "ddp/fused/bf16", "ddp/overlap/bf16", "ddp/torch/fp32", "fsdp/fused/fp32",
-                 "fsdp/fused/bf16"]
+                 "fsdp/fused/bf16", "fsdp/overlap/bf16"]
 
 
 @pytest.fixture(scope="module")
@@ -211,8 +213,9 @@ WIDE = {name: json.load(open(os.path.join(GOLDEN, name)))
 WIDE_RUNS = {  # (golden file, ranks, backend, variants, extra env)
     "cfg5_gloo2": ("cfg5_golden.json", 2, "gloo", ["fsdp/fused/fp32", "fsdp/fused/bf16", "fsdp/torch/fp32"], {}),
     "cfg5_rccl1": ("cfg5_golden.json", 1, "nccl", ["fsdp/fused/fp32", "fsdp/fused/bf16"], {}),
-    "cfg4_gloo2": ("cfg4_golden.json", 2, "gloo", ["fsdp/fused/fp32", "fsdp/fused/bf16", "fsdp/torch/fp32"], {}),
-    "cfg4_rccl1": ("cfg4_golden.json", 1, "nccl", ["fsdp/fused/fp32", "fsdp/fused/bf16"], {}),
+    "cfg4_gloo2": ("cfg4_golden.json", 2, "gloo", ["fsdp/fused/fp32", "fsdp/fused/bf16", "fsdp/overlap/bf16",
+                                                    "fsdp/torch/fp32"], {}),
+    "cfg4_rccl1": ("cfg4_golden.json", 1, "nccl", ["fsdp/fused/fp32", "fsdp/fused/bf16", "fsdp/overlap/bf16"], {}),
     "ddp124_gloo2": ("ddp124_golden.json", 2, "gloo", ["ddp/fused/fp32", "ddp/fused/bf16", "ddp/overlap/bf16",
                                                         "ddp/torch/fp32"], {"BUCKET_MB": "25"}),
     "ddp124_rccl1": ("ddp124_golden.json", 1, "nccl", ["ddp/fused/bf16", "ddp/overlap/bf16"], {"BUCKET_MB": "25"}),
