@@ -249,8 +249,8 @@ GPT2MI_EXPORT int gpt2mi_gemm(int layout, int epilogue, int M, int N, int K, con
   hipStream_t s = (hipStream_t)stream;
   // the ping-pong kernel takes any M, N multiple of 64 (a partial last tile; GPT-2 1.5B's 1600 / 4800) and any K-tile
   // count >= 2; the 2-stage 256x256 kernel full column tiles only
-  // (transposed operands — layouts 1 / 2 — full tiles only: the partial-tile reads of an m-contiguous operand run
-  // past its rows, which gpt2mi_gemm_wgrad's callers allocate for and this entry's do not)
+  // (transposed operands — layouts 1 / 2 — full column tiles only here; since ABI v11 a partial tile's m-contiguous
+  // reads stop at the operand's last element (gemm_pp.hip BND), which only gpt2mi_gemm_wgrad's launches exercise)
   const bool pp_ok = splits == 1 && epilogue != EPI_ATOMIC &&
                      (layout == 0 || (N % 256 == 0 && (layout == 1 || M % 256 == 0)));
   const bool big_ok = pp_ok && N % 256 == 0 && (layout <= 1 || M % 256 == 0);

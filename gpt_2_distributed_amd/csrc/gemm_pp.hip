@@ -424,6 +424,11 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
   // DYN: the queue counter's old value from this block's latest grab (thread 0; written by an asm atomic, so that no
   // compiler-inserted vmcnt(0) drains the DMAs for its return; valid once a wait has retired it: read only at the end of
   // the main loop, after its vmcnt(0) waits). The first grab (for the block's second tile) goes out before the prologue.
+  // The compiler cannot see that the return register is written late: tests/test_gemm_grab_hazard.py walks the emitted
+  // code of every DYN kernel and checks that no instruction touches that register before a vmcnt(0) retires the atomic.
+  // (A compiler-visible __hip_atomic_fetch_add is turned into a wave-reduced atomic followed at once by vmcnt(0),
+  // which would drain the epilogue's stores and the next tile's DMAs at every grab.) The labels assume that blocks with
+  // equal blockIdx.x % 8 share an XCD: a speed assumption only, each label's counter being private to its blocks.
   [[maybe_unused]] unsigned grab = 0u;
   [[maybe_unused]] auto grab_next = [&]() {
     if (threadIdx.x == 0) {

@@ -22,8 +22,8 @@ Outputs (all small data files, no reference source):
                     T=256, 2 ranks x B=1, grad_accum=2, 2 steps, lr 1e-4, Zipf tokens stored in the file: the FSDP +
                     gradient-accumulation test of the 1.5B configuration.
   ddp124_golden.json the same identity at cfg 3's widths (GPT-2 124M: C=768, H=12, V=50257, T=1024) on 2 layers,
-                    2 ranks x B=2, grad_accum=1, 3 steps, lr 1e-3, Zipf tokens stored in the file: the DDP test with
-                    the default 64 MiB buckets.
+                    2 ranks x B=2, grad_accum=1, 3 steps, lr 1e-3, Zipf tokens stored in the file: the DDP test (the
+                    wrapper runs it with its default 25 MiB buckets, torch DDP's bucket_cap_mb).
   cfg4_golden.json  the same identity at BASELINE cfg 4's widths (GPT-2 350M: C=1024, H=16, V=50257, T=1024) on 2
                     layers, 2 ranks x B=1, grad_accum=2, 3 steps, lr 1e-3, Zipf tokens stored in the file: the FSDP
                     (FULL_SHARD) test of the 350M configuration (train_gpt2_distributed.py:146-161).
