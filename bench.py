@@ -85,6 +85,8 @@ def main():
     # optimizer step over grad_accum micro-batches of --batch sequences per rank
     ap.add_argument("--parallel", choices=["ddp", "fsdp"], default="ddp", help="multi-rank wrapper (N > 1)")
     ap.add_argument("--grad_accum", type=int, default=1)
+    ap.add_argument("--reshard", action="store_true",
+                    help="--parallel fsdp: reshard_after_forward (FULL_SHARD's memory behaviour; default: resident units)")
     ap.add_argument("--probe-every", type=int, default=5,
                     help="time the probed kernel launches (HIP events) in every N-th timed step")
     args = ap.parse_args()
@@ -109,7 +111,8 @@ def main():
         from gpt_2_distributed_amd.parallel import DistributedDataParallel, ShardedDataParallel
         wrap = ShardedDataParallel if args.parallel == "fsdp" else DistributedDataParallel
         # the embeddings' all-reduce (DDP) / reduce-scatter (FSDP) runs under the optimizer step of every other range
-        ddp = wrap(model, bucket_mb=args.bucket_mb, overlap_optimizer=True)
+        extra = dict(reshard_after_forward=True) if args.parallel == "fsdp" and args.reshard else {}
+        ddp = wrap(model, bucket_mb=args.bucket_mb, overlap_optimizer=True, **extra)
         opt = ddp.configure_optimizers(learning_rate=1e-4)
         fwd = ddp
     else:
@@ -224,7 +227,8 @@ def main():
         "data": "synthetic (uniform random tokens, resident in HBM)",
         "config": {"workload": f"GPT-2 {args.model} training step: fwd+loss+bwd+AdamW"
                                + ({"ddp": " + bucketed grad all-reduce in the backward",
-                                   "fsdp": " + per-block FSDP all-gather / reduce-scatter"}[args.parallel]
+                                   "fsdp": " + per-block FSDP all-gather / reduce-scatter"
+                                   + (", resharded after forward" if args.reshard else "")}[args.parallel]
                                   if wrapped else "")
                                + f", dropout {args.dropout}" + (f", {GA} accumulated micro-batches" if GA > 1 else ""),
                    "model": f"GPT-2 {args.model}", "global_batch": B * world * GA, "seq_len": T,

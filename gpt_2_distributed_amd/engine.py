@@ -302,6 +302,10 @@ class GradHooks:
     def fwd_unit(self, unit: str) -> None:
         """FSDP: the parameters of ``unit`` ("embed", "h.<l>", "head") are about to be read."""
 
+    def bwd_unit(self, unit: str) -> None:
+        """FSDP (reshard_after_forward): the backward of ``unit`` is about to run: its parameters are read again and its
+        gradients (and the fc2 bias gradient of the unit before it, which this unit's LayerNorm backward forms) written."""
+
 
 class Engine:
     """Owns the workspaces, the bf16 weight shadow and the grad arena of one GPT2 model."""
@@ -341,6 +345,9 @@ class Engine:
         self.base_seed = 1234
         self.grad_sync: Optional[GradHooks] = None  # set by data-parallel wrappers (parallel.py)
         self.param_provider = None  # FSDP: owns the full parameter views (gathers them per unit)
+        # FullyShardedDataParallel(reshard_after_forward=True): the storage of every parameter / shadow / gradient view
+        # (the resident units' slots instead of the full arenas, which are then freed); None: the full arenas
+        self.store = None
         self.grad_dirty = False     # the grad arena holds gradients of an earlier backward (accumulation)
         # the weight-gradient GEMMs of the running backward write their slots outright: set by a full backward
         # that starts from zero_grad(set_to_none=True), which then zeroes only the accumulated slots
@@ -392,15 +399,35 @@ class Engine:
         K.gemm_wgrad_kt(*a, sched=self._wgrad_sched(), **kw)
 
     # ---- parameter views ------------------------------------------------------------------------------
+    def _loc(self, kind, name):
+        """(storage, element offset) of ``name``'s slot in the fp32 parameters ("p"), the bf16 shadow ("w16"), the W^T
+        shadow ("wT") or the fp32 gradients ("g"): the full arenas, or the storage of the unit that holds it now
+        (FullyShardedDataParallel(reshard_after_forward=True), engine.store)."""
+        off = self.layout.slots[name].offset
+        if self.store is not None:
+            buf, base = self.store.loc(kind, name)
+            return buf, off - base
+        return {"p": self.model.arena, "g": self.grad, "w16": self.shadow, "wT": self.shadowT}[kind], off
+
+    def _flat(self, kind, name):
+        buf, o = self._loc(kind, name)
+        return buf[o:o + self.layout.slots[name].reserved]
+
     def p(self, name):  # fp32 master view
-        return self.layout.view(self.model.arena, name)
+        buf, o = self._loc("p", name)
+        s = self.layout.slots[name]
+        return buf[o:o + s.numel].view(s.shape)
 
     def g(self, name):  # fp32 grad view
-        return self.layout.view(self.grad, name)
+        buf, o = self._loc("g", name)
+        s = self.layout.slots[name]
+        return buf[o:o + s.numel].view(s.shape)
+
+    def gpad(self, name, rows):  # fp32 grad view of the whole (padded) slot, [rows, cols]
+        return self._flat("g", name).view(rows, -1)
 
     def w16(self, name):  # bf16 shadow view (flat)
-        s = self.layout.slots[name]
-        return self.shadow[s.offset:s.offset + s.reserved]
+        return self._flat("w16", name)
 
     def refresh_shadow(self):
         """bf16 copy of the fp32 master weights the GEMMs read. The fused optimizer rewrites it in its
@@ -429,29 +456,30 @@ class Engine:
         sl = self.layout.slots[name]
         return self._rows(name) % 64 == 0 and sl.shape[1] % 64 == 0
 
-    def refresh_shadowT(self, names=None):
+    def refresh_shadowT(self, names=None, shadow=None, shadowT=None, base=0):
         """Transpose every (or the listed) 2-D weight of the bf16 shadow into shadowT in one launch
-        (49 separate 64x64-tile launches cost 0.28 ms per step)."""
-        key = tuple(names) if names is not None else None
+        (49 separate 64x64-tile launches cost 0.28 ms per step). shadow / shadowT / base: the bf16 storage of one
+        unit whose first element is arena element ``base`` (FSDP's reshard slots) instead of the full shadows."""
+        key = (tuple(names) if names is not None else None, base)
         if key not in self._tdesc_cache:
             rows, tiles = [], 0
             for n in (self._t_weights if names is None else [m for m in names if m in self._t_weights]):
                 if self.wT_ok(n):
                     sl = self.layout.slots[n]
                     R, Cc = self._rows(n), sl.shape[1]
-                    rows.append((sl.offset, R, Cc, tiles))
+                    rows.append((sl.offset - base, R, Cc, tiles))
                     tiles += (R // 64) * (Cc // 64)
             self._tdesc_cache[key] = (torch.tensor(rows, dtype=torch.int64, device=self.device) if rows else None,
                                       len(rows), tiles)
         desc, n, tiles = self._tdesc_cache[key]
         if n:
-            K.transpose_bf16_batched(self.shadow, self.shadowT, desc, n, tiles)
+            K.transpose_bf16_batched(self.shadow if shadow is None else shadow,
+                                     self.shadowT if shadowT is None else shadowT, desc, n, tiles)
         if names is None:
             self._shadowT_stale = False
 
     def wT16(self, name):  # bf16 W^T view (flat, [in][out_padded])
-        s = self.layout.slots[name]
-        return self.shadowT[s.offset:s.offset + s.reserved]
+        return self._flat("wT", name)
 
     def _sync_shadows(self, act, need_grad):
         if self.param_provider is not None:
@@ -466,14 +494,24 @@ class Engine:
         if self.param_provider is not None:
             self.param_provider.fwd_unit(unit)
 
+    def _unit_bwd(self, unit):
+        if self.param_provider is not None:
+            self.param_provider.bwd_unit(unit)
+
     # ---- grads ---------------------------------------------------------------------------------------
     def bind_grads(self):
+        if self.store is not None:
+            return  # reshard_after_forward: the module's parameters have no storage; gradients live in the store
         for name, p in self.params_by_name.items():
             if name == "lm_head.weight":
                 continue
             p.grad = self.layout.view(self.grad, name)
 
     def zero_grad(self):
+        if self.store is not None:  # reshard_after_forward: the next backward starts from zero (Engine._prepare_grads)
+            self._grad_dead = True
+            self.grad_dirty = False
+            return
         K.zero_(self.grad)
         self.grad_dirty = False
         self._grad_dead = False
@@ -490,20 +528,25 @@ class Engine:
         # (gemm_wgrad / EPI_F32; not the EPI_ATOMIC fallback of widths that are not multiples of 64)
         return act == BF16 and self.cfg.n_embd % 64 == 0
 
+    def acc_ranges(self, lo, hi, shift=0):
+        """(offset - lo + shift, count) of the arena ranges in [lo, hi) outside the GEMM-written weight slots (wte with
+        its pad rows, the four matrices of every block): the LayerNorm params, biases, wpe, ln_f and the alignment gaps,
+        which the backward accumulates into and so starts from zero."""
+        gemm = sorted((max(sl.offset, lo), min(sl.offset + sl.reserved, hi)) for n, sl in self.layout.slots.items()
+                      if n in self._t_weights and sl.offset < hi and sl.offset + sl.reserved > lo)
+        rng, pos = [], lo
+        for a, b in gemm:
+            if a > pos:
+                rng.append((pos - lo + shift, a - pos))
+            pos = max(pos, b)
+        if pos < hi:
+            rng.append((pos - lo + shift, hi - pos))
+        return rng
+
     def _zero_accumulated(self):
-        """Zero the arena outside the GEMM-written weight slots (wte with its pad rows, the four matrices of
-        every block): LayerNorm params, biases, wpe, ln_f and the alignment gaps, in one launch."""
+        """Zero the arena outside the GEMM-written weight slots in one launch."""
         if self._acc_ranges is None:
-            gemm = sorted((sl.offset, sl.offset + sl.reserved) for n, sl in self.layout.slots.items()
-                          if n in self._t_weights)
-            rng, pos = [], 0
-            for a, b in gemm:
-                if a > pos:
-                    rng.append((pos, a - pos))
-                pos = max(pos, b)
-            if pos < self.grad.numel():
-                rng.append((pos, self.grad.numel() - pos))
-            self._acc_ranges = torch.tensor(rng, dtype=torch.int64).to(self.device)
+            self._acc_ranges = torch.tensor(self.acc_ranges(0, self.grad.numel()), dtype=torch.int64).to(self.device)
         K.zero_ranges(self.grad, self._acc_ranges)
 
     def _prepare_grads(self, full_backward_act=None):
@@ -512,6 +555,14 @@ class Engine:
         forms EVERY weight gradient (the whole-model loss backward): its GEMMs then write the weight slots
         and only the rest of the arena is zeroed."""
         self._grad_fresh = False
+        if self.store is not None:
+            # reshard_after_forward: every backward starts from zero (the previous one's gradients were reduce-scattered
+            # into the shard); the store zeroes the root unit's gradients now and each block's as its slot is assigned
+            self._grad_fresh = full_backward_act is not None and self._lazy_zero_ok(full_backward_act)
+            self.store.begin_grads(self._grad_fresh)
+            self._grad_dead = False
+            self.grad_dirty = False
+            return
         if self._grad_dead or all(p.grad is None for p in self.params_by_name.values()):
             self._grad_dead = False
             if full_backward_act is not None and self._lazy_zero_ok(full_backward_act):
@@ -579,8 +630,7 @@ class Engine:
         (wte as its zero-padded [Vp, C] slot for the tied lm_head)."""
         if act == BF16:
             return self.w16(name)
-        s = self.layout.slots[name]
-        return self.model.arena[s.offset:s.offset + s.reserved]
+        return self._flat("p", name)
 
     def _grad_enabled(self):
         return torch.is_grad_enabled() and any(p.requires_grad for p in self._params)
@@ -750,14 +800,17 @@ class Engine:
         M = B * T
         x = ws.x
         # ln_f backward starts the residual gradient; emits the fc2 branch grad of the last block
+        self._unit_bwd("head")
         K.layernorm_bwd(x[L], self.p("transformer.ln_f.weight"), ws.mf, ws.rf, ws.dln, ws.dres,
                         self.g("transformer.ln_f.weight"), self.g("transformer.ln_f.bias"), ws.dres_bf,
                         self.g(f"transformer.h.{L-1}.mlp.fc2.bias"), M, C, pr, seeds[("fc2", L - 1)], dres_init=True)
         self._ready("head")
         for l in reversed(range(L)):
+            self._unit_bwd(f"h.{l}")
             self._block_bwd(l, ws.blocks[l], ws, x[l], B, T, act, pr, pa, seeds, last=(l == 0))
             self._ready(f"h.{l}")
         # embedding backward: atomics into the tied wte grad (the lm_head wgrad already wrote it)
+        self._unit_bwd("embed")
         K.embed_bwd(idx, ws.dres, self.g("transformer.wte.weight"), self.g("transformer.wpe.weight"), B, T, C, pr,
                     seeds["embd"], T_valid=sv.T)
         self._ready("embed")
@@ -832,7 +885,7 @@ class Engine:
         with self._probe("lm_head_dgrad"):
             self._dgrad(act, M, ws.dln, ws.dlogits, "transformer.wte.weight", C, Vp, K.EPI_BF16, alpha_dev=alpha_dev,
                         alpha=gs)
-        wte_g = self.layout.padded_view(self.grad, "transformer.wte.weight", Vp)
+        wte_g = self.gpad("transformer.wte.weight", Vp)
         with self._probe("lm_head_wgrad"), self._probe("wgrad"):
             if C % 64 == 0 and act == BF16 and M % 128 == 0 and Vp % 256 == 0:
                 # dwte^T = lnf^T . dlogits with lnf transposed once (0.1 GB at cfg 2): one transposed GEMM operand
@@ -890,6 +943,9 @@ class Engine:
         """kind: "block" (x = residual stream, model.py:213-219), "mlp" (x = ln2 output, model.py:186-192),
         "attn" (x = ln1 output, model.py:110-159). Returns (y, saved state)."""
         self.gemm_sched = self.base_sched  # (a backward that raised midway left its flags)
+        if self.store is not None:
+            raise NotImplementedError("sub-module calls under FullyShardedDataParallel(reshard_after_forward=True): "
+                                      "call the wrapped model")
         cfg = self.cfg
         C = cfg.n_embd
         if x.dim() != 3 or x.shape[-1] != C:

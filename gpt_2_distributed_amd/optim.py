@@ -123,8 +123,8 @@ class FusedAdamW(_FlatAdamW):
 
 class ShardedAdamW(_FlatAdamW):
     """One launch per FSDP unit: each writes its unit's bf16 shard straight into that unit's all-gather buffer
-    (FullyShardedDataParallel.bf16_chunk), so the next forward gathers in place, and its grad-norm partial sums into
-    its slice of one buffer, finalised once into the clip_grad_norm_ value."""
+    (FullyShardedDataParallel.bf16_chunk; only while the model computes in bf16), so the next forward gathers in place,
+    and its grad-norm partial sums into its slice of one buffer, finalised once into the clip_grad_norm_ value."""
 
     def __init__(self, fsdp, lr=1e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1):
         super().__init__([fsdp.flat_param], fsdp.flat_param, lr, betas, eps, weight_decay)
@@ -154,8 +154,9 @@ class ShardedAdamW(_FlatAdamW):
             q = f.plans[i]
             if q.name == tail:
                 f.wait_tail()
-            self._run(p, f.grad_shard, f.bf16_chunk(q.name), q.soff, q.soff + q.per, self.unit_partials[i * P:(i + 1) * P])
-        f.mark_params_updated(bf16_fresh=True)
+            pb = f.bf16_chunk(q.name) if f.wants_bf16() else None  # (fp32 FSDP gathers fp32: no bf16 shards)
+            self._run(p, f.grad_shard, pb, q.soff, q.soff + q.per, self.unit_partials[i * P:(i + 1) * P])
+        f.mark_params_updated(bf16_fresh=f.wants_bf16())
         # the clip_grad_norm_(inf) value of the full model: sum of squares over units (one finalisation) and shards
         K.norm_finalize(self.unit_partials, self.unit_partials.numel(), self.grad_norm)
         if f.coll:

@@ -21,7 +21,8 @@ Replaces the reference's ``DDP(model, device_ids=[device])`` / ``FSDP(model, ...
   moments live only on the owning rank. In the forward the engine asks for each unit just before it
   reads it; the wrapper all-gathers that unit in the compute precision (bf16 under autocast, like
   MixedPrecision(param_dtype=bf16)) and has the following units' all-gathers already in flight on RCCL's
-  stream (by default every remaining unit's, issued at the first unit: ``prefetch_depth``). In the backward each unit's gradient range is reduce-scattered (bf16
+  stream, as many as fit a byte budget of gathered output (``prefetch_bytes``, like FSDP's ``limit_all_gathers``
+  rate limiter; ``prefetch_depth`` caps it by a unit count). In the backward each unit's gradient range is reduce-scattered (bf16
   under autocast, like reduce_dtype=bf16) the moment the engine marks it final, overlapped with the
   remaining backward. MI355X-first difference: a gathered unit stays resident until the next optimizer
   step (288 GB HBM holds every unit of every BASELINE model), so the backward does not re-gather it and
@@ -338,6 +339,10 @@ class _FSDPHooks(_DPHooks):
     def fwd_unit(self, unit):
         self.fsdp._gather_for(unit)
 
+    def bwd_unit(self, unit):
+        if self.fsdp.store is not None:
+            self.fsdp._bwd_unit(unit)
+
     def inflight(self) -> bool:
         # an all-gather or reduce-scatter this wrapper issued has not completed yet (a host-side event query: when it
         # reads complete, the collective is certainly done before anything enqueued now runs; while the host runs ahead
@@ -345,21 +350,188 @@ class _FSDPHooks(_DPHooks):
         f = self.fsdp
         if not f.coll:
             return False
-        return any(w is not None and u not in f._fenced and not w.is_completed() for u, (w, _) in f._pending.items()) or \
+        return any(w is not None and u not in f._fenced and not w.is_completed() for u, (w, *_) in f._pending.items()) or \
             any(w is not None and not w.is_completed() for _, w, _ in f._rs_works) or \
             (f._tail is not None and f._tail[1] is not None and not f._tail[1].is_completed())
+
+
+def fsdp_memory_plan(units, world: int, reshard: bool) -> dict:
+    """Per-rank bytes of FullyShardedDataParallel over ``units`` (unit_ranges) at ``world`` ranks, bf16 autocast:
+    sharded state (fp32 master, grad, two AdamW moments, bf16 shard: 18 B per sharded element), compute views and
+    collective staging. Resident: every unit's views (12 B/param: fp32 params + bf16 shadow + W^T + fp32 grads) and
+    every unit's bf16 gather / reduce-scatter buffers. reshard_after_forward: the root unit's views, _ReshardStore's
+    P_SLOTS parameter slots (8 B/param of a block) and G_SLOTS gradient slots (4 B), STAGE_SLOTS-deep bf16 gather and
+    reduce-scatter rings of one block plus the root's own buffers, and a bf16 reduce-scatter output per unit."""
+    plans, shard_total = plan_shards(units, world)
+    sharded = shard_total * (4 + 4 + 8 + 2)
+    total = units[-1][2]
+    if not reshard:
+        views = total * (4 + 2 + 2 + 4)
+        staging = sum(p.per * world for p in plans) * (2 + 2)
+    else:
+        root = [p for p in plans if p.name in ("embed", "head")]
+        blocks = [p for p in plans if p.name not in ("embed", "head")]
+        nb = max((p.n for p in blocks), default=0)
+        per_b = max((p.per for p in blocks), default=0)
+        views = sum(p.n for p in root) * (4 + 2 + 2 + 4) + \
+            _ReshardStore.P_SLOTS * nb * (4 + 2 + 2) + _ReshardStore.G_SLOTS * nb * 4
+        staging = 2 * FullyShardedDataParallel.STAGE_SLOTS * per_b * world * 2 + \
+            sum(p.per * world for p in root) * (2 + 2) + shard_total * 2
+    return {"sharded_state_bytes": sharded, "compute_view_bytes": views, "staging_bytes": staging,
+            "total": sharded + views + staging}
+
+
+class _ReshardStore:
+    """FullyShardedDataParallel(reshard_after_forward=True): where the engine's parameter, shadow and gradient views
+    live (Engine.store). The root unit (embed + head: wte, wpe, ln_f; used at both ends of the step, and kept gathered
+    as torch FSDP keeps its root) has compact resident storage. Every GPT2Block unit borrows one of P_SLOTS parameter
+    slots (fp32 parameters, bf16 shadow, bf16 W^T) while it is gathered — the forward of the next units and the
+    backward evict it, so the backward gathers it again — and one of G_SLOTS gradient slots from the start of its
+    backward until its reduce-scatter has packed the gradient. The compute views are then root + 2 blocks of
+    parameters + 3 blocks of gradients per rank instead of the whole model, and the per-rank total shrinks with the
+    world size (memory_report). Slot reuse is safe in stream order: a slot is refilled only after every kernel that
+    reads its previous unit has been enqueued on the compute stream."""
+
+    P_SLOTS = 2
+    G_SLOTS = 3
+
+    def __init__(self, fsdp):
+        from . import _lib as K
+        eng, lay, plan = fsdp.engine, fsdp.module.layout, fsdp.plan
+        dev = fsdp.flat_param.device
+        self.K, self.eng, self.plan = K, eng, plan
+        e, h = plan["embed"], plan["head"]
+        self.root_base = {"embed": e.lo, "head": h.lo - e.n}  # head stored right after embed
+        nr = e.n + h.n
+        kinds = (("p", torch.float32), ("w16", torch.bfloat16), ("wT", torch.bfloat16), ("g", torch.float32))
+        self.root = {k: torch.zeros(nr, dtype=dt, device=dev) for k, dt in kinds}
+        self.blocks = [u for u in fsdp.order if u not in self.root_base]
+        self.nb = max(plan[u].n for u in self.blocks) if self.blocks else 0
+        self.pslots = [{k: torch.zeros(self.nb, dtype=dt, device=dev) for k, dt in kinds[:3]}
+                       for _ in range(self.P_SLOTS)]
+        self.gslots = [torch.zeros(self.nb, dtype=torch.float32, device=dev) for _ in range(self.G_SLOTS)]
+        self.p_of: Dict[str, int] = {}
+        self.p_owner: List[Optional[str]] = [None] * self.P_SLOTS
+        self.p_next = 0
+        self.g_of: Dict[str, int] = {}
+        self.g_owner: List[Optional[str]] = [None] * self.G_SLOTS
+        self.unit_of = {}
+        for name, sl in lay.slots.items():
+            self.unit_of[name] = next(u for u in fsdp.order if plan[u].lo <= sl.offset < plan[u].hi)
+        dt = torch.int64
+        self.acc_root = torch.tensor(eng.acc_ranges(e.lo, e.hi, 0) + eng.acc_ranges(h.lo, h.hi, e.n), dtype=dt).to(dev)
+        self.acc_block = {u: torch.tensor(eng.acc_ranges(plan[u].lo, plan[u].hi), dtype=dt).to(dev)
+                          for u in self.blocks}
+        self.fresh = False
+        self.evicted = None  # callback(unit): a block unit lost its parameter slot
+
+    # -- the engine's views --
+    def loc(self, kind, name):
+        u = self.unit_of[name]
+        if u in self.root_base:
+            return self.root[kind], self.root_base[u]
+        if kind == "g":
+            i = self.g_of.get(u)
+            if i is None:
+                raise RuntimeError(f"reshard_after_forward: {u} has no gradient slot (its backward has not started)")
+            return self.gslots[i], self.plan[u].lo
+        i = self.p_of.get(u)
+        if i is None:
+            raise RuntimeError(f"reshard_after_forward: {u} is not gathered")
+        return self.pslots[i][kind], self.plan[u].lo
+
+    # -- parameter slots --
+    def take_pslot(self, u) -> dict:
+        """The parameter slot of block unit u (its own if it still has one, else the next one round-robin, evicting
+        its previous unit)."""
+        i = self.p_of.get(u)
+        if i is None:
+            i = self.p_next
+            self.p_next = (i + 1) % self.P_SLOTS
+            old = self.p_owner[i]
+            if old is not None:
+                del self.p_of[old]
+                if self.evicted is not None:
+                    self.evicted(old)
+            self.p_owner[i] = u
+            self.p_of[u] = i
+        return self.pslots[i]
+
+    def unit_params(self, u):
+        """(fp32, bf16, W^T storage, arena element of storage element 0) for unpacking gathered unit u."""
+        p = self.plan[u]
+        if u in self.root_base:
+            o = p.lo - self.root_base[u]
+            return self.root["p"][o:o + p.n], self.root["w16"][o:o + p.n], self.root["w16"], self.root["wT"], \
+                self.root_base[u]
+        sl = self.take_pslot(u)
+        return sl["p"][:p.n], sl["w16"][:p.n], sl["w16"], sl["wT"], p.lo
+
+    # -- gradient slots --
+    def begin_grads(self, fresh: bool):
+        """A backward starts: its gradients start from zero (the weight-gradient GEMMs write their slots when fresh,
+        every other range is zeroed)."""
+        self.fresh = fresh
+        self.g_of.clear()
+        self.g_owner = [None] * self.G_SLOTS
+        if fresh:
+            self.K.zero_ranges(self.root["g"], self.acc_root)
+        else:
+            self.K.zero_(self.root["g"])
+
+    def take_gslot(self, u):
+        if u in self.root_base or u in self.g_of:
+            return
+        i = next((k for k, o in enumerate(self.g_owner) if o is None), None)
+        if i is None:
+            raise RuntimeError("reshard_after_forward: every gradient slot is in use")
+        self.g_owner[i] = u
+        self.g_of[u] = i
+        g = self.gslots[i]
+        if self.fresh:
+            self.K.zero_ranges(g, self.acc_block[u])
+        else:
+            self.K.zero_(g)
+
+    def release_gslot(self, u):
+        i = self.g_of.pop(u, None)
+        if i is not None:
+            self.g_owner[i] = None
+
+    def unit_grad(self, u) -> torch.Tensor:
+        p = self.plan[u]
+        if u in self.root_base:
+            o = p.lo - self.root_base[u]
+            return self.root["g"][o:o + p.n]
+        return self.gslots[self.g_of[u]][:p.n]
+
+    def view_bytes(self) -> int:
+        return sum(t.numel() * t.element_size() for t in self.root.values()) + \
+            sum(t.numel() * t.element_size() for sl in self.pslots for t in sl.values()) + \
+            sum(t.numel() * t.element_size() for t in self.gslots)
 
 
 class FullyShardedDataParallel(nn.Module):
     """FULL_SHARD data parallelism over per-GPT2Block units (see the module docstring)."""
 
-    # the forward unit (index in arena order: embed, h.0, h.1, h.2, ...) at which every pending all-gather is waited for
-    FENCE_UNIT = 3
+    # gathered bytes (the all-gathers' outputs, every rank's chunk) in flight ahead of the unit being computed: a GPT-2
+    # 124M block is 14 MB in bf16, 350M 25 MB, 1.5B 61 MB, so 512 MiB keeps the whole 124M model, 20 350M blocks or 8
+    # 1.5B blocks ahead (at 8 ranks a 1.5B block takes ~0.4 ms of ring all-gather over xGMI against ~1.4 ms of forward
+    # compute per block at B = 32), and bounds what a rank receives before it computes
+    PREFETCH_BYTES = 512 << 20
 
     def __init__(self, module, device_ids=None, bucket_mb: float = 64.0, prefetch: bool = True,
-                 prefetch_depth: Optional[int] = None, overlap_optimizer: bool = False):
+                 prefetch_depth: Optional[int] = None, overlap_optimizer: bool = False,
+                 prefetch_bytes: Optional[int] = None, reshard_after_forward: bool = False):
         super().__init__()
         self.module = module
+        # reshard_after_forward: FULL_SHARD's memory behaviour (torch FSDP's default for FULL_SHARD, which the
+        # reference runs, train_gpt2_distributed.py:146-161): a GPT2Block unit's gathered parameters are released
+        # after its forward and gathered again for its backward, its gradient lives only until its reduce-scatter, and
+        # the full-model compute views are freed (_ReshardStore). Off (default): every gathered unit stays resident
+        # until the next optimizer step (no re-gather: 288 GB holds every BASELINE model's views).
+        self.reshard_after_forward = bool(reshard_after_forward)
+        self.store: Optional[_ReshardStore] = None
         # overlap_optimizer (with configure_optimizers' ShardedAdamW): the backward returns with the last unit's
         # reduce-scatter (the embeddings, final only after the embedding backward) in flight, and the optimizer updates
         # every other unit under it; flat_param.grad of that unit is final after optimizer.step() or
@@ -372,10 +544,12 @@ class FullyShardedDataParallel(nn.Module):
         self.world = dist.get_world_size()
         self.rank = dist.get_rank()
         self.prefetch = prefetch
-        # units gathered ahead of the one being computed (None: every remaining unit at the first unit's forward, so the
-        # gathers finish under the first blocks and the rest of the forward runs with no collective in flight; a
-        # gathered unit stays resident until the next optimizer step either way, so depth costs no memory)
+        # the all-gathers kept in flight ahead of the unit being computed: as many following units as fit
+        # prefetch_bytes of gathered output (None: PREFETCH_BYTES), at most prefetch_depth units (None: no unit cap);
+        # each unit's forward first retires the gathers that have completed (an event query), and waits only for its
+        # own, so the GEMMs run the static persistent schedule exactly while no gather is in flight (GradHooks.inflight)
         self.prefetch_depth = prefetch_depth
+        self.prefetch_bytes = self.PREFETCH_BYTES if prefetch_bytes is None else int(prefetch_bytes)
         W, r = self.world, self.rank
         self.coll = use_collectives(W)
         if self.coll:
@@ -396,12 +570,16 @@ class FullyShardedDataParallel(nn.Module):
         self._bufs: Dict[tuple, torch.Tensor] = {}
         self._valid: Dict[str, Optional[torch.dtype]] = {u: None for u in self.order}
         self._pending: Dict[str, tuple] = {}       # unit -> (work, dtype) of an in-flight all-gather
-        # pending all-gathers the compute stream already waits for (fenced at unit FENCE_UNIT of the forward): no kernel
-        # enqueued after the fence can overlap them, so they do not count as in flight for the GEMM schedule
+        # pending all-gathers the compute stream already waits for (retired once their event reads complete): no
+        # kernel enqueued after that wait can overlap them, so they do not count as in flight for the GEMM schedule
         self._fenced = set()
         self._rs_works: List[tuple] = []            # (unit, work, out) of in-flight reduce-scatters
         # every unit's bf16_chunk == bf16(its flat_param range) (set by our AdamW, which writes them)
         self._bf16_fresh = False
+        self._compute_dtype: Optional[torch.dtype] = None  # of the latest forward (None before the first)
+        self._stage_next = {}                      # reshard: next slot of each staging ring
+        self._stage_user: Dict[tuple, Optional[str]] = {}  # reshard: (ring, slot) -> unit whose data it holds
+        self._rs_slot_work: Dict[int, object] = {}  # reshard: rs ring slot -> the reduce-scatter that reads it
         self._seen_version = None
         self.hooks = _FSDPHooks(self, W)
         # a torch optimizer on flat_param (fused AdamW does not bump its version): every gathered unit goes stale
@@ -411,6 +589,14 @@ class FullyShardedDataParallel(nn.Module):
         eng.param_provider = self.hooks
         eng.zero_grad()
         eng.bind_grads()
+        if self.reshard_after_forward:
+            self.store = _ReshardStore(self)
+            self.store.evicted = self._evicted
+            eng.store = self.store
+            # the full-model views are freed (as FSDP frees the unsharded FlatParameter): the module's own parameters
+            # keep their shapes but no storage; every view the engine forms comes from the store
+            for t in (module.arena, eng.shadow, eng.shadowT, eng.grad):
+                t.untyped_storage().resize_(0)
 
     # ---- parameters: the flat shard only (torch optimizers / clip_grad_norm_ see what FSDP exposes) ----
     def parameters(self, recurse: bool = True):
@@ -420,16 +606,20 @@ class FullyShardedDataParallel(nn.Module):
         yield (prefix + ("." if prefix else "") + "flat_param", self.flat_param)
 
     def memory_report(self) -> dict:
-        """Bytes per rank: sharded state (fp32 master, grad, AdamW moments, bf16 AG source) vs the
-        resident compute views (fp32 params, bf16 shadow + transposed shadow, transient fp32 grad arena,
-        collective staging). DDP keeps every one of the sharded tensors whole."""
-        n_full = self.module.arena.numel()
-        sharded = self.shard_total * (4 + 4 + 8 + 2)
-        views = n_full * (4 + 2 + 2 + 4)
-        staging = sum(t.numel() * t.element_size() for t in self._bufs.values())
-        return {"params": n_full, "world": self.world, "sharded_state_bytes": sharded,
+        """Bytes per rank: sharded state (fp32 master, grad, AdamW moments, bf16 AG source) vs the compute views (fp32
+        params, bf16 shadow + transposed shadow, transient fp32 gradients) and the collective staging, as allocated now;
+        ``per_rank_bytes_by_world``: the same model at other world sizes (fsdp_memory_plan). DDP keeps every one of the
+        sharded tensors whole. Resident mode: the views cover the whole model on every rank; reshard_after_forward: the
+        root unit plus the store's block slots, so the per-rank total falls with the world size."""
+        n_full = self.module.layout.total
+        rs = self.store is not None
+        views = self.store.view_bytes() if rs else n_full * (4 + 2 + 2 + 4)
+        return {"params": n_full, "world": self.world, "reshard_after_forward": rs,
+                "sharded_state_bytes": self.shard_total * (4 + 4 + 8 + 2),
                 "ddp_equivalent_state_bytes": n_full * (4 + 4 + 8),
-                "compute_view_bytes": views, "staging_bytes": staging}
+                "compute_view_bytes": views,
+                "staging_bytes": sum(t.numel() * t.element_size() for t in self._bufs.values()),
+                "per_rank_bytes_by_world": {w: fsdp_memory_plan(self.units, w, rs)["total"] for w in (1, 2, 4, 8)}}
 
     # ---- buffers ------------------------------------------------------------------------------------
     def _buf(self, kind, unit, dtype, n):
@@ -441,10 +631,19 @@ class FullyShardedDataParallel(nn.Module):
         return t
 
     def bf16_chunk(self, unit) -> torch.Tensor:
-        """This rank's bf16 shard of ``unit``: its chunk of the unit's all-gather buffer, so the bf16 gather runs in
-        place (RCCL copies nothing locally; at one rank the gathered unit IS the shard). The optimizer writes it."""
+        """This rank's bf16 shard of ``unit``. Resident mode: its chunk of the unit's all-gather buffer, so the bf16
+        gather runs in place (RCCL copies nothing locally; at one rank the gathered unit IS the shard).
+        reshard_after_forward: its range of one shard-sized bf16 buffer (the gathers go to staging rings). The
+        optimizer writes it."""
         p = self.plan[unit]
+        if self.store is not None:
+            return self._buf("shard16", None, torch.bfloat16, self.shard_total)[p.soff:p.soff + p.per]
         return self._buf("ag", unit, torch.bfloat16, p.per * self.world)[self.rank * p.per:(self.rank + 1) * p.per]
+
+    def wants_bf16(self) -> bool:
+        """The optimizer should write the bf16 shards: the latest forward computed in bf16 (autocast), or none ran yet.
+        In fp32 mode no bf16 gather buffer is allocated or written (a later bf16 forward re-rounds every shard)."""
+        return self._compute_dtype in (None, torch.bfloat16)
 
     # ---- forward: per-unit all-gather with prefetch ---------------------------------------------------
     def mark_params_updated(self, bf16_fresh: bool):
@@ -463,64 +662,146 @@ class FullyShardedDataParallel(nn.Module):
             self._bf16_fresh = False
             self._seen_version = self.flat_param._version
 
+    # reshard_after_forward: staging rings (block units' gathers and reduce-scatter inputs); a slot is refilled only
+    # after its previous unit's consumer (the unpack, or the reduce-scatter) is enqueued / waited for
+    STAGE_SLOTS = 3
+
+    def _ring(self, ring, dtype, n):
+        """The next slot of staging ring ``ring`` (STAGE_SLOTS buffers of n elements): (index, buffer)."""
+        i = self._stage_next.get(ring, 0)
+        self._stage_next[ring] = (i + 1) % self.STAGE_SLOTS
+        return i, self._buf(ring, i, dtype, n)
+
+    def _ring_free(self, ring) -> bool:
+        """The next slot of ``ring`` holds no gathered unit still waiting for its unpack."""
+        i = self._stage_next.get(ring, 0)
+        return self._stage_user.get((ring, i)) not in self._pending
+
     def _issue_gather(self, unit, dtype):
         from . import _lib as K
         p = self.plan[unit]
-        out = self._buf("ag", unit, dtype, p.per * self.world)
+        n = p.per * self.world
+        if self.store is not None and unit in self.store.blocks:
+            ring = "ag16" if dtype == torch.bfloat16 else "ag32"
+            i, out = self._ring(ring, dtype, self._block_ag_len())
+            out = out[:n]
+            self._stage_user[(ring, i)] = unit
+        else:
+            out = self._buf("ag", unit, dtype, n)
         if dtype == torch.bfloat16:
             if not self._bf16_fresh:  # a step we did not run (torch optimizer, load): re-round every shard
                 fp = self.flat_param.detach()
                 for q in self.plans:
                     K.cast_f32_bf16(fp[q.soff:q.soff + q.per], self.bf16_chunk(q.name), q.per)
                 self._bf16_fresh = True
-            src = self.bf16_chunk(unit)  # in place: a view of out
+            src = self.bf16_chunk(unit)  # resident mode: a view of out (in place)
         else:
             src = self.flat_param.detach()[p.soff:p.soff + p.per]
         if not self.coll:
-            if src.data_ptr() != out.data_ptr():
-                out.copy_(src)
+            if src.data_ptr() != out[self.rank * p.per:].data_ptr():
+                out[self.rank * p.per:(self.rank + 1) * p.per].copy_(src)
             work = None
         else:
             work = dist.all_gather_into_tensor(out, src, async_op=True)
-        self._pending[unit] = (work, dtype)
+        self._pending[unit] = (work, dtype, out)
         self._fenced.discard(unit)  # a new gather of the unit: not waited for yet
 
-    def _gather_for(self, unit):
+    def _block_ag_len(self) -> int:
+        return max(self.plan[u].per for u in self.store.blocks) * self.world
+
+    def _gather_for(self, unit, backward=False):
+        """Make ``unit``'s parameters readable in the compute precision: wait for (or issue) its all-gather and unpack
+        it, with the next units' gathers issued under this unit's compute (forward order, or backward order)."""
         from . import _lib as K
         eng = self.engine
-        dtype = eng.compute_dtype()
+        dtype = eng.compute_dtype() if not backward else self._compute_dtype
+        self._compute_dtype = dtype
         self._check_version()
         if self._valid.get(unit) != dtype:
             if unit not in self._pending or self._pending[unit][1] != dtype:
                 self._issue_gather(unit, dtype)
         if self.prefetch:  # the next units' all-gathers ride under this unit's compute
-            i = self.order.index(unit)
-            last = len(self.order) if self.prefetch_depth is None else min(len(self.order), i + 1 + self.prefetch_depth)
-            for nxt in self.order[i + 1:last]:
-                if self._valid.get(nxt) != dtype and nxt not in self._pending:
-                    self._issue_gather(nxt, dtype)
-        if self.coll and self.order.index(unit) >= min(self.FENCE_UNIT, len(self.order) - 1):
-            # every gather still pending is waited for here (a stream wait): they were issued at the first unit and are
-            # done by now at any world size, so this costs nothing, and the rest of the forward's GEMMs keep the static
-            # persistent schedule (GradHooks.inflight) instead of the work-queue variant
-            for u, (w, _) in self._pending.items():
-                if w is not None and u not in self._fenced:
-                    w.wait()
-                    self._fenced.add(u)
+            self._prefetch_after(unit, dtype, backward)
+        if self.coll:
+            self._retire_completed()
         if self._valid.get(unit) == dtype:
             return
-        work, _ = self._pending.pop(unit)
+        work, _, out = self._pending.pop(unit)
         if work is not None and unit not in self._fenced:
             work.wait()
         self._fenced.discard(unit)
         p = self.plan[unit]
-        out = self._buf("ag", unit, dtype, p.per * self.world)
-        bf = eng.shadow[p.lo:p.hi] if dtype == torch.bfloat16 else None
-        K.fsdp_unpack(out, self.module.arena[p.lo:p.hi], bf, p.n)
-        if dtype == torch.bfloat16:
-            names = [n for n, s in self.module.layout.slots.items() if p.lo <= s.offset < p.hi]
-            eng.refresh_shadowT(names)
+        if self.store is not None:
+            f32, b16, b16_all, t16_all, base = self.store.unit_params(unit)
+            K.fsdp_unpack(out, f32, b16 if dtype == torch.bfloat16 else None, p.n)
+            if dtype == torch.bfloat16:
+                names = [n for n, s in self.module.layout.slots.items() if p.lo <= s.offset < p.hi]
+                eng.refresh_shadowT(names, shadow=b16_all, shadowT=t16_all, base=base)
+        else:
+            bf = eng.shadow[p.lo:p.hi] if dtype == torch.bfloat16 else None
+            K.fsdp_unpack(out, self.module.arena[p.lo:p.hi], bf, p.n)
+            if dtype == torch.bfloat16:
+                names = [n for n, s in self.module.layout.slots.items() if p.lo <= s.offset < p.hi]
+                eng.refresh_shadowT(names)
         self._valid[unit] = dtype
+
+    def _evicted(self, unit):
+        """reshard_after_forward: block ``unit`` lost its parameter slot (its next use gathers it again)."""
+        self._valid[unit] = None
+
+    def _bwd_unit(self, unit):
+        """reshard_after_forward: before ``unit``'s backward: its parameters gathered again (the next unit in backward
+        order prefetched), and gradient slots for it and for the block before it, whose fc2 bias gradient this unit's
+        first LayerNorm backward forms (the head's: the last block's)."""
+        st = self.store
+        if unit != "embed":
+            self._gather_for(unit, backward=True)
+        i = self.order.index(unit)
+        if unit in st.blocks:
+            st.take_gslot(unit)
+        if i > 0 and self.order[i - 1] in st.blocks:
+            st.take_gslot(self.order[i - 1])
+
+    def _gather_bytes(self, unit, dtype) -> int:
+        p = self.plan[unit]
+        return p.per * self.world * torch.empty((), dtype=dtype).element_size()
+
+    def _prefetch_after(self, unit, dtype, backward=False):
+        """Issue the all-gathers of the units after ``unit`` (forward order; backward order for a backward re-gather)
+        while the gathered bytes in flight stay within prefetch_bytes (and the units ahead within prefetch_depth); one
+        unit ahead is always allowed. reshard_after_forward: at most STAGE_SLOTS - 1 block gathers wait for their
+        unpack (the staging ring), and a unit is gathered ahead only if it will need it (not resident)."""
+        seq = self.order if not backward else list(reversed(self.order))
+        i = seq.index(unit)
+        ahead = seq[i + 1:]
+        if backward:
+            ahead = [u for u in ahead if u != "embed"]  # the root stays gathered
+        if self.prefetch_depth is not None:
+            ahead = ahead[:self.prefetch_depth]
+        if self.store is not None:
+            ahead = ahead[:self.STAGE_SLOTS - 1]
+        inflight = sum(self._gather_bytes(u, dt) for u, (_, dt, _) in self._pending.items() if u != unit)
+        for k, nxt in enumerate(ahead):
+            if self._valid.get(nxt) == dtype:
+                continue
+            if nxt in self._pending:
+                continue
+            nb = self._gather_bytes(nxt, dtype)
+            if k > 0 and inflight + nb > self.prefetch_bytes:
+                break
+            if self.store is not None and nxt in self.store.blocks and \
+                    not self._ring_free("ag16" if dtype == torch.bfloat16 else "ag32"):
+                break
+            self._issue_gather(nxt, dtype)
+            inflight += nb
+
+    def _retire_completed(self):
+        """Stream-wait every pending all-gather whose work reads complete (costs nothing: it is done) so that it stops
+        counting as in flight; the rest stay pending until they complete or their unit runs."""
+        for u, (w, *_) in self._pending.items():
+            if w is not None and u not in self._fenced and w.is_completed():
+                w.wait()
+                self._fenced.add(u)
 
     # ---- backward: per-unit reduce-scatter as ranges become final ----------------------------------------
     def _reduce_scatter(self, unit):
@@ -528,14 +809,35 @@ class FullyShardedDataParallel(nn.Module):
         p = self.plan[unit]
         eng = self.engine
         dtype = eng.bwd_act  # reduce_dtype = the compute precision (bf16 under autocast)
-        inp = self._buf("rs_in", unit, dtype, p.per * self.world)
-        K.fsdp_pack(eng.grad[p.lo:p.hi], inp, p.n, p.per * self.world)
-        # in place: this rank's chunk of the packed input receives the reduced shard (RCCL copies nothing locally)
-        out = inp[self.rank * p.per:(self.rank + 1) * p.per]
+        n = p.per * self.world
+        slot = None
+        if self.store is not None and unit in self.store.blocks:
+            # reshard_after_forward: the packed input goes to a staging ring (its slot's previous reduce-scatter waited
+            # for first), the reduced shard to a shard-sized buffer of the unit; the gradient slot is free once packed
+            ring = "rs16" if dtype == torch.bfloat16 else "rs32"
+            i, inp = self._ring(ring, dtype, self._block_ag_len())
+            inp = inp[:n]
+            prev = self._rs_slot_work.pop((ring, i), None)
+            if prev is not None:
+                prev.wait()
+            slot = (ring, i)
+            out = self._buf("rs_out", unit, dtype, p.per)
+            K.fsdp_pack(self.store.unit_grad(unit), inp, p.n, n)
+            self.store.release_gslot(unit)
+        else:
+            inp = self._buf("rs_in", unit, dtype, n)
+            src = self.store.unit_grad(unit) if self.store is not None else eng.grad[p.lo:p.hi]
+            K.fsdp_pack(src, inp, p.n, n)
+            # in place: this rank's chunk of the packed input receives the reduced shard (RCCL copies nothing locally)
+            out = inp[self.rank * p.per:(self.rank + 1) * p.per]
         if not self.coll:
+            if out.data_ptr() != inp[self.rank * p.per:].data_ptr():
+                out.copy_(inp[self.rank * p.per:(self.rank + 1) * p.per])
             work = None
         else:
             work = dist.reduce_scatter_tensor(out, inp, op=dist.ReduceOp.SUM, async_op=True)
+            if slot is not None:
+                self._rs_slot_work[slot] = work
         self._rs_works.append((unit, work, out))
 
     def _finish_reduce(self):
@@ -580,6 +882,10 @@ class FullyShardedDataParallel(nn.Module):
 
     @contextlib.contextmanager
     def no_sync(self):
+        if self.store is not None:
+            # unsharded gradients would have to outlive their unit's backward (the reference loop accumulates without
+            # no_sync, reduce-scattering every micro-step into the sharded gradient, which this mode does)
+            raise NotImplementedError("no_sync() with reshard_after_forward=True: accumulate without no_sync")
         old = self.hooks.sync
         self.hooks.sync = False
         try:
@@ -616,7 +922,7 @@ class FullyShardedDataParallel(nn.Module):
     def full_arena(self) -> torch.Tensor:
         """The fp32 master parameters of every unit, all-gathered (FULL_STATE_DICT; fixes the reference's
         rank-0-only early return before this collective, train_gpt2_distributed.py:81-94)."""
-        arena = torch.zeros_like(self.module.arena)
+        arena = torch.zeros(self.module.layout.total, dtype=torch.float32, device=self.flat_param.device)
         for p in self.plans:
             src = self.flat_param.detach()[p.soff:p.soff + p.per]
             out = torch.empty(p.per * self.world, dtype=torch.float32, device=arena.device)
@@ -637,14 +943,18 @@ class FullyShardedDataParallel(nn.Module):
     @torch.no_grad()
     def load_full_state_dict(self, sd):
         m = self.module
-        for n, p in m.named_parameters():
-            p.copy_(sd[n])
+        lay = m.layout
+        arena = torch.zeros(lay.total, dtype=torch.float32, device=self.flat_param.device)
+        for n in lay.slots:
+            lay.view(arena, n).copy_(sd[n])
+        if self.store is None:  # the module's own views (resident mode keeps them)
+            m.arena.copy_(arena)
         for pl in self.plans:
             a, b = pl.lo + self.rank * pl.per, min(pl.hi, pl.lo + (self.rank + 1) * pl.per)
             chunk = self.flat_param.detach()[pl.soff:pl.soff + pl.per]
             chunk.zero_()
             if b > a:
-                chunk[:b - a].copy_(m.arena[a:b])
+                chunk[:b - a].copy_(arena[a:b])
         self.mark_params_updated(False)
         self._seen_version = None  # force a refresh at the next forward
 

@@ -61,6 +61,9 @@ def build_parser():
     p.add_argument("--synthetic_tokens", type=int, default=2_000_000)
     p.add_argument("--resume", type=str, default="", help="checkpoint step_XXXXXXX directory to resume from")
     p.add_argument("--log_every", type=int, default=20)
+    p.add_argument("--fsdp_reshard", action="store_true",
+                   help="fsdp: release each block's gathered parameters after its forward (FULL_SHARD's memory "
+                        "behaviour) instead of keeping them resident until the optimizer step")
     return p
 
 
@@ -180,7 +183,7 @@ def main(argv=None):
     if args.training_mode == "ddp":
         model = DistributedDataParallel(base, overlap_optimizer=True)  # the grad norm comes from the fused AdamW
     elif args.training_mode == "fsdp":
-        model = FullyShardedDataParallel(base, overlap_optimizer=True)
+        model = FullyShardedDataParallel(base, overlap_optimizer=True, reshard_after_forward=args.fsdp_reshard)
     else:
         model = base
     optim = model.configure_optimizers(weight_decay=0.1, learning_rate=args.lr, betas=(0.9, 0.95))

@@ -20,6 +20,9 @@ Variants (one torch.distributed.run launch runs them all):
                 the next backward must overwrite the grad shard, not add to the stale one
   fsdp/ckpt     fsdp save_checkpoint -> fresh model + wrapper -> load_checkpoint -> the next step equals
                 the uninterrupted run's
+  fsdp/reshard  FullyShardedDataParallel(reshard_after_forward=True): FULL_SHARD's memory behaviour (each block's
+                gathered parameters released after its forward and gathered again for its backward, gradients only
+                until their reduce-scatter, the full-model views freed)
 
 The same worker runs three production-width goldens (tests/golden/make_golden.py, the reference itself on the
 concatenated batch, Zipf tokens stored in the file):
@@ -62,9 +65,9 @@ else:
     toks = torch.randint(0, 509, (S, GA, w * P, 65), generator=torch.Generator().manual_seed(5))
 BUCKET_MB = float(os.environ.get("BUCKET_MB", "0.25"))
 
-def build(mode, opt_kind, overlap=False):
+def build(mode, opt_kind, overlap=False, reshard=False):
     m = GPT2(cfg).to("cuda:0")
-    wrap = FullyShardedDataParallel(m, overlap_optimizer=overlap) if mode == "fsdp" else \
+    wrap = FullyShardedDataParallel(m, overlap_optimizer=overlap, reshard_after_forward=reshard) if mode == "fsdp" else \
         DistributedDataParallel(m, bucket_mb=BUCKET_MB, overlap_optimizer=overlap)
     if opt_kind == "torch":
         opt = torch.optim.AdamW(wrap.parameters(), lr=G["lr"], weight_decay=0.1, betas=(0.9, 0.95), fused=True)
@@ -104,7 +107,7 @@ res = {}
 for variant in os.environ["VARIANTS"].split(","):
     mode, kind, prec = variant.split("/")
     opt_kind = "torch" if kind == "torch" else "fused"
-    m, wrap, opt = build(mode, opt_kind, overlap=kind == "overlap")
+    m, wrap, opt = build(mode, opt_kind, overlap=kind == "overlap", reshard=kind == "reshard")
     losses, norms = [], []
     if kind == "ckpt":
         step(wrap, opt, 0, prec, opt_kind, False)
@@ -131,7 +134,8 @@ dist.barrier(); dist.destroy_process_group()
 
 VARIANTS = ["ddp/fused/fp32", "ddp/fused/bf16", "ddp/overlap/fp32", "ddp/torch/fp32", "ddp/nosync/fp32",
             "fsdp/overlap/fp32", "fsdp/fused/fp32",
-            "fsdp/fused/bf16", "fsdp/torch/fp32", "fsdp/ckpt/bf16", "ddp/ckpt/fp32"]
+            "fsdp/fused/bf16", "fsdp/torch/fp32", "fsdp/ckpt/bf16", "ddp/ckpt/fp32", "fsdp/reshard/fp32",
+            "fsdp/reshard/bf16"]
 
 
 def _launch(tmp, nproc, variants, port, golden="ddp_golden.json", **env_extra):
@@ -155,7 +159,7 @@ def results(tmp_path_factory):
 
 
 RCCL_VARIANTS = ["ddp/fused/fp32", "ddp/fused/bf16", "ddp/overlap/bf16", "ddp/torch/fp32", "fsdp/fused/fp32",
-                 "fsdp/fused/bf16", "fsdp/overlap/bf16"]
+                 "fsdp/fused/bf16", "fsdp/overlap/bf16", "fsdp/reshard/bf16"]
 
 
 @pytest.fixture(scope="module")
@@ -211,10 +215,11 @@ def test_rccl_collectives_vs_reference(rccl_results, variant):
 WIDE = {name: json.load(open(os.path.join(GOLDEN, name)))
         for name in ("cfg5_golden.json", "cfg4_golden.json", "ddp124_golden.json")}
 WIDE_RUNS = {  # (golden file, ranks, backend, variants, extra env)
-    "cfg5_gloo2": ("cfg5_golden.json", 2, "gloo", ["fsdp/fused/fp32", "fsdp/fused/bf16", "fsdp/torch/fp32"], {}),
+    "cfg5_gloo2": ("cfg5_golden.json", 2, "gloo", ["fsdp/fused/fp32", "fsdp/fused/bf16", "fsdp/torch/fp32",
+                                                    "fsdp/reshard/fp32", "fsdp/reshard/bf16"], {}),
     "cfg5_rccl1": ("cfg5_golden.json", 1, "nccl", ["fsdp/fused/fp32", "fsdp/fused/bf16"], {}),
     "cfg4_gloo2": ("cfg4_golden.json", 2, "gloo", ["fsdp/fused/fp32", "fsdp/fused/bf16", "fsdp/overlap/bf16",
-                                                    "fsdp/torch/fp32"], {}),
+                                                    "fsdp/torch/fp32", "fsdp/reshard/fp32", "fsdp/reshard/bf16"], {}),
     "cfg4_rccl1": ("cfg4_golden.json", 1, "nccl", ["fsdp/fused/fp32", "fsdp/fused/bf16", "fsdp/overlap/bf16"], {}),
     "ddp124_gloo2": ("ddp124_golden.json", 2, "gloo", ["ddp/fused/fp32", "ddp/fused/bf16", "ddp/overlap/bf16",
                                                         "ddp/torch/fp32"], {"BUCKET_MB": "25"}),
@@ -278,3 +283,18 @@ def test_fsdp_memory_report(results):
     mem = results["fsdp/fused/bf16"]["mem"]
     print("fsdp memory per rank:", mem)
     assert mem["sharded_state_bytes"] < 0.6 * mem["ddp_equivalent_state_bytes"]
+
+
+def test_fsdp_reshard_memory_report(results, wide_results):
+    """reshard_after_forward (FULL_SHARD's memory behaviour) on live wrappers: the compute views the store allocated are
+    the ones fsdp_memory_plan prices (root unit + parameter / gradient slots), independent of the world size, and the
+    planned per-rank total falls with it (tests/test_fsdp_schedule_cpu.py prices the BASELINE models)."""
+    from gpt_2_distributed_amd.parallel import _ReshardStore
+    for res in (results, wide_results["cfg4_gloo2"], wide_results["cfg5_gloo2"]):
+        rs, rd = res["fsdp/reshard/bf16"]["mem"], res["fsdp/fused/bf16"]["mem"]
+        print("reshard:", rs, "\nresident:", rd)
+        assert rs["reshard_after_forward"] and not rd["reshard_after_forward"]
+        assert rs["sharded_state_bytes"] == rd["sharded_state_bytes"]
+        w = {int(k): v for k, v in rs["per_rank_bytes_by_world"].items()}
+        assert w[1] > w[2] > w[4] > w[8]
+        assert _ReshardStore.P_SLOTS == 2 and _ReshardStore.G_SLOTS == 3

@@ -1,0 +1,44 @@
+#!/bin/bash
+# Round 5: the whole GPU test suite + smoke, the default bench, BASELINE cfg 5 as SURVEY specifies it (GPT-2 1.5B, FSDP,
+# B = 32, grad_accum 4; resident and resharded) on one forced-RCCL rank, and rocprof summaries of the default bench and
+# of GPT-2 1.5B at B = 8 -> gpurun_out/$TAG/
+set -o pipefail
+T=${TAG:-r5c}
+O=gpurun_out/$T
+mkdir -p $O
+export TMPDIR=/tmp
+if [ -z "$SKIP_TESTS" ]; then
+  timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread > $O/pytest_gpu.log 2>&1
+  rc=$?; tail -3 $O/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { cat $O/smoke.log; exit 1; }
+  tail -2 $O/smoke.log
+fi
+run() {  # name, timeout, command...
+  local name=$1 lim=$2; shift 2
+  timeout -k 10 $lim "$@" > $O/$name.log 2>&1
+  local rc=$?
+  grep '^{' $O/$name.log | tail -1 > $O/$name.json
+  echo "$name rc=$rc $(cut -c1-240 $O/$name.json)"
+  return $rc
+}
+TR="python -m torch.distributed.run --nnodes=1 --nproc-per-node=1 --master-addr=127.0.0.1 --master-port=29581"
+run bench 300 python bench.py || exit $?
+if [ -n "$MODELS" ]; then
+  run m15b_fsdp_ga4 600 env GPT2MI_FORCE_COLLECTIVES=1 $TR bench.py --no-cpu-baseline --parallel fsdp --model 1.5B \
+    --batch 32 --grad_accum 4 --steps 4 --warmup 2 || exit $?
+  run m15b_fsdp_ga4_reshard 600 env GPT2MI_FORCE_COLLECTIVES=1 $TR bench.py --no-cpu-baseline --parallel fsdp \
+    --reshard --model 1.5B --batch 32 --grad_accum 4 --steps 4 --warmup 2 || exit $?
+fi
+if [ -n "$PROF" ]; then
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python bench.py --steps 5 --warmup 3 \
+    --no-cpu-baseline > $O/prof.log 2>&1 || exit $?
+  python tools/rocpd_stats.py $O/prof/run_results.db $O/kernel_stats.csv && \
+    python tools/prof_summary.py $O/kernel_stats.csv 8 > $O/summary.txt 2>&1; head -30 $O/summary.txt
+fi
+if [ -n "$PROF15" ]; then
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof15 -o run -- python bench.py --model 1.5B --batch 8 \
+    --steps 3 --warmup 2 --no-cpu-baseline > $O/prof15.log 2>&1 || exit $?
+  grep '^{' $O/prof15.log | tail -1 > $O/m15b8.json
+  python tools/rocpd_stats.py $O/prof15/run_results.db $O/kernel_stats15.csv && \
+    python tools/prof_summary.py $O/kernel_stats15.csv 3 > $O/summary15.txt 2>&1; head -30 $O/summary15.txt
+fi
