@@ -130,9 +130,14 @@ def main():
     GA = args.grad_accum
 
     def step(i):
-        for a in range(GA):  # the reference loop (:400-425): no_sync on all but the last micro-step
+        # the reference loop (:400-425) runs every micro-step's backward synced; the resident wrappers skip the
+        # collective on all but the last one (no_sync: the same sums), the resharded FSDP reduce-scatters every one
+        # as the reference does (its gradients do not outlive their unit's backward)
+        sync_each = args.parallel == "fsdp" and args.reshard
+        for a in range(GA):
             x, y = batches[(i * GA + a) % len(batches)]
-            ctx = fwd.no_sync() if (a + 1 < GA and hasattr(fwd, "no_sync")) else contextlib.nullcontext()
+            ctx = fwd.no_sync() if (a + 1 < GA and hasattr(fwd, "no_sync") and not sync_each) \
+                else contextlib.nullcontext()
             with ctx:
                 with torch.autocast("cuda", dtype=torch.bfloat16):  # the reference trainer's step (:404)
                     _, loss = fwd(x, labels=y)
