@@ -45,8 +45,16 @@ __global__ __launch_bounds__(256) void transpose_bf16_batched_kernel(const bf16*
                                                                     bf16* __restrict__ dst,
                                                                     const int64_t* __restrict__ desc, int n) {
   const int64_t tile = blockIdx.x;
-  int i = 0;
-  while (i + 1 < n && desc[4 * (i + 1) + 3] <= tile) ++i;  // n <= a few hundred: scalar loop
+  // the matrix holding this tile: the last i with first_tile(i) <= tile (binary search over the sorted first tiles:
+  // GPT-2 1.5B has 193 matrices, and a linear scan of dependent scalar loads per block took the 1.5B refresh to 2.8 ms,
+  // 2.1 TB/s, against 4.6 TB/s at 124M's 49)
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (desc[4 * mid + 3] <= tile) lo = mid;
+    else hi = mid - 1;
+  }
+  const int i = lo;
   const int64_t off = desc[4 * i], R = desc[4 * i + 1], C = desc[4 * i + 2], t = tile - desc[4 * i + 3];
   const int tc = (int)(C / TT);
   transpose_tile(src + off, dst + off, (int)(t / tc) * TT, (int)(t % tc) * TT, (int)C, (int)R);

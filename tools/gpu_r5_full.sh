@@ -23,6 +23,16 @@ run() {  # name, timeout, command...
 }
 TR="python -m torch.distributed.run --nnodes=1 --nproc-per-node=1 --master-addr=127.0.0.1 --master-port=29581"
 run bench 300 python bench.py || exit $?
+if [ -n "$WRAPPED" ]; then  # the one-rank DDP / FSDP overhead against the same call's bench
+  run ddp1 300 env GPT2MI_FORCE_COLLECTIVES=1 $TR bench.py --no-cpu-baseline --parallel ddp || exit $?
+  run fsdp1 300 env GPT2MI_FORCE_COLLECTIVES=1 $TR bench.py --no-cpu-baseline --parallel fsdp || exit $?
+  run fsdp1_reshard 300 env GPT2MI_FORCE_COLLECTIVES=1 $TR bench.py --no-cpu-baseline --parallel fsdp --reshard || exit $?
+  run bench_again 300 python bench.py --no-cpu-baseline || exit $?
+fi
+if [ -n "$RESHARD15" ]; then
+  run m15b_fsdp_ga4_reshard 600 env GPT2MI_FORCE_COLLECTIVES=1 $TR bench.py --no-cpu-baseline --parallel fsdp \
+    --reshard --model 1.5B --batch 32 --grad_accum 4 --steps 4 --warmup 2 || exit $?
+fi
 if [ -n "$MODELS" ]; then
   run m15b_fsdp_ga4 600 env GPT2MI_FORCE_COLLECTIVES=1 $TR bench.py --no-cpu-baseline --parallel fsdp --model 1.5B \
     --batch 32 --grad_accum 4 --steps 4 --warmup 2 || exit $?
