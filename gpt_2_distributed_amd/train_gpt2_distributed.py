@@ -228,7 +228,10 @@ def main(argv=None):
             x = x.to(device, non_blocking=True)
             y = y.to(device, non_blocking=True)
             last = (micro + 1) % args.grad_accum_steps == 0
-            ctx = model.no_sync() if (hasattr(model, "no_sync") and not last) else _Null()
+            # no_sync on the resident wrappers (the same sums, one collective per step); the resharded FSDP syncs every
+            # micro-step, as the reference's loop does for every mode (its gradients do not outlive their unit)
+            ctx = model.no_sync() if (hasattr(model, "no_sync") and not last
+                                      and not getattr(model, "reshard_after_forward", False)) else _Null()
             with ctx:
                 with torch.autocast("cuda", dtype=torch.bfloat16):  # as train_gpt2_distributed.py:404
                     _, loss = model(x, labels=y)

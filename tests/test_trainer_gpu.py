@@ -156,3 +156,32 @@ def test_trainer_cli_end_to_end(tmp_path):
         assert 0 < s["gpu_utilization_pct"] < 100 and s["cpu_mb"] > 0 and s["epoch_time"] > 0
     for st in ("step_0000002", "step_0000003"):
         assert (ckpt / st / "model.pt").exists() and (ckpt / st / "optim.pt").exists()
+
+
+@pytest.mark.parametrize("mode", ["ddp", "fsdp", "fsdp_reshard"])
+def test_trainer_cli_wrapped_one_rank_resume(tmp_path, mode):
+    """The trainer under torchrun in the reference's ddp / fsdp modes (one rank, RCCL collectives forced on), with
+    --fsdp_reshard (FULL_SHARD's memory behaviour: every micro-step reduce-scatters, no no_sync), 2 micro-batches
+    per step: 2 steps + a resume for 2 more log the losses of 4 uninterrupted steps (the sharded checkpoint:
+    model.pt gathered on rank 0, optim_rank{r}.pt per rank)."""
+    data = tmp_path / "data"
+    mode_args = ["--training_mode", "fsdp", "--fsdp_reshard"] if mode == "fsdp_reshard" else ["--training_mode", mode]
+    port = {"ddp": 29571, "fsdp": 29572, "fsdp_reshard": 29573}[mode]
+    base = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1", "--master-addr=127.0.0.1",
+            f"--master-port={port}", "-m", "gpt_2_distributed_amd.train_gpt2_distributed", "--data_dir", str(data),
+            "--synthetic", "2", "--synthetic_tokens", "60000", "--seq_len", "128", "--batch", "4", "--model", "124M",
+            "--grad_accum_steps", "2", "--workers", "0", "--log_every", "1", *mode_args]
+    env = dict(os.environ, GPT2MI_FORCE_COLLECTIVES="1")
+    r = subprocess.run(base + ["--max_steps", "4", "--save_every", "2", "--save_dir", str(tmp_path / "a")], cwd=REPO,
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    full = {json.loads(l)["step"]: json.loads(l)["loss"] for l in r.stdout.splitlines() if l.startswith("{")}
+    assert sorted(full) == [1, 2, 3, 4] and all(0.0 < v < 20.0 for v in full.values()), full
+    ck = tmp_path / "a" / "step_0000002"
+    assert (ck / "model.pt").exists() and ((ck / "optim_rank0.pt").exists() if mode != "ddp" else (ck / "optim.pt").exists())
+    r = subprocess.run(base + ["--max_steps", "4", "--save_every", "100", "--save_dir", str(tmp_path / "b"),
+                               "--resume", str(ck)], cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    resumed = {json.loads(l)["step"]: json.loads(l)["loss"] for l in r.stdout.splitlines() if l.startswith("{")}
+    for s in (3, 4):
+        assert abs(resumed[s] - full[s]) <= 1e-4 * full[s], (s, resumed, full)
