@@ -50,5 +50,5 @@ if [ -n "$PROF15" ]; then
     --steps 3 --warmup 2 --no-cpu-baseline > $O/prof15.log 2>&1 || exit $?
   grep '^{' $O/prof15.log | tail -1 > $O/m15b8.json
   python tools/rocpd_stats.py $O/prof15/run_results.db $O/kernel_stats15.csv && \
-    python tools/prof_summary.py $O/kernel_stats15.csv 3 > $O/summary15.txt 2>&1; head -30 $O/summary15.txt
+    python tools/prof_summary.py $O/kernel_stats15.csv 5 > $O/summary15.txt 2>&1; head -30 $O/summary15.txt
 fi
