@@ -52,3 +52,9 @@ if [ -n "$PROF15" ]; then
   python tools/rocpd_stats.py $O/prof15/run_results.db $O/kernel_stats15.csv && \
     python tools/prof_summary.py $O/kernel_stats15.csv 5 > $O/summary15.txt 2>&1; head -30 $O/summary15.txt
 fi
+if [ -n "$TRAIN" ]; then  # the reference trainer's loop end to end on synthetic Zipf shards: the loss curve
+  timeout -k 10 600 python -m gpt_2_distributed_amd.train_gpt2_distributed --synthetic 4 --synthetic_tokens 20000000 \
+    --seq_len 1024 --batch 16 --grad_accum_steps 4 --max_steps 300 --log_every 10 --save_every 100000 --lr 6e-4 \
+    --workers 2 --save_dir /tmp/ckpt_train > $O/train_curve.log 2>&1 || { tail -20 $O/train_curve.log; exit 1; }
+  grep '^{' $O/train_curve.log | python -c "import json,sys; r=[json.loads(l) for l in sys.stdin]; print('train', [(d['step'], d['loss']) for d in r][::3], 'tok/s', r[-1]['tok_per_s_node'])"
+fi
