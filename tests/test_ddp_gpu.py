@@ -106,8 +106,8 @@ def fingerprint(wrap):
 res = {}
 for variant in os.environ["VARIANTS"].split(","):
     mode, kind, prec = variant.split("/")
-    opt_kind = "torch" if kind == "torch" else "fused"
-    m, wrap, opt = build(mode, opt_kind, overlap=kind == "overlap", reshard=kind in ("reshard", "ckptrs"))
+    opt_kind = "torch" if kind in ("torch", "rstorch") else "fused"
+    m, wrap, opt = build(mode, opt_kind, overlap=kind == "overlap", reshard=kind in ("reshard", "ckptrs", "rstorch"))
     losses, norms = [], []
     if kind in ("ckpt", "ckptrs", "ckptx"):  # ckptrs: saved and resumed resharded; ckptx: resident -> resharded
         step(wrap, opt, 0, prec, opt_kind, False)
@@ -135,7 +135,7 @@ dist.barrier(); dist.destroy_process_group()
 VARIANTS = ["ddp/fused/fp32", "ddp/fused/bf16", "ddp/overlap/fp32", "ddp/torch/fp32", "ddp/nosync/fp32",
             "fsdp/overlap/fp32", "fsdp/fused/fp32",
             "fsdp/fused/bf16", "fsdp/torch/fp32", "fsdp/ckpt/bf16", "ddp/ckpt/fp32", "fsdp/reshard/fp32",
-            "fsdp/reshard/bf16", "fsdp/ckptrs/bf16", "fsdp/ckptx/fp32"]
+            "fsdp/reshard/bf16", "fsdp/ckptrs/bf16", "fsdp/ckptx/fp32", "fsdp/rstorch/fp32"]
 
 
 def _launch(tmp, nproc, variants, port, golden="ddp_golden.json", **env_extra):
@@ -187,7 +187,7 @@ def _check_vs_golden(r, variant, GOLD=GOLD, world=2):
     rn = np.abs(np.array(r["norms"]) - GOLD["grad_norms"]) / np.array(GOLD["grad_norms"])
     # torch's clip_grad_norm_ on FSDP's flat shard is the local shard's norm (the reference's FSDP quirk, SURVEY §5
     # iv): only a world of one reports the global norm there; DDP's and the fused optimizer's are global
-    if not (variant.startswith("fsdp/torch") and world > 1):
+    if not (variant.startswith("fsdp/") and "torch" in variant.split("/")[1] and world > 1):
         assert rn.max() < t_norm, (variant, r["norms"], GOLD["grad_norms"])
     fp32 = variant.endswith("fp32")
     tot, tot_ref = 0.0, 0.0
