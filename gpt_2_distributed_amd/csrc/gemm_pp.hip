@@ -1040,13 +1040,17 @@ int num_cus() {
 }
 
 // persistent variant: one block per CU, grid a multiple of 8
+#ifndef GPT2MI_PERSIST_GRID
+#define GPT2MI_PERSIST_GRID 0  // A/B builds: a fixed persistent grid (a CU-masked stream's CU count), 0 = every CU
+#endif
+GPT2MI_PRODUCT_KNOB(GPT2MI_PERSIST_GRID, 0);
 template <int EPI>
 int launch_persistent(const GemmParams& Pin, hipStream_t s, bool dyn) {
   static std::atomic<unsigned> next_slot{0};
   GemmParams P = Pin;
   P.qslot = (int)(next_slot.fetch_add(1u, std::memory_order_relaxed) % kQueueSlots);
   const int ntiles = ((P.M + BM - 1) / BM) * (P.N / BN);  // N % 256 == 0 (gemm_pp_dispatch)
-  dim3 grid(min(ntiles, num_cus()));
+  dim3 grid(min(ntiles, GPT2MI_PERSIST_GRID > 0 ? GPT2MI_PERSIST_GRID : num_cus()));
   if (dyn) gemm_pp_kernel<false, false, EPI, 0, true, false, true><<<grid, kThreads, 0, s>>>(P);
   else gemm_pp_kernel<false, false, EPI, 0, true><<<grid, kThreads, 0, s>>>(P);
   return gpt2mi::check_launch("gemm_pp_persistent");
