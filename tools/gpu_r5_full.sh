@@ -58,3 +58,9 @@ if [ -n "$TRAIN" ]; then  # the reference trainer's loop end to end on synthetic
     --workers 2 --save_dir /tmp/ckpt_train > $O/train_curve.log 2>&1 || { tail -20 $O/train_curve.log; exit 1; }
   grep '^{' $O/train_curve.log | python -c "import json,sys; r=[json.loads(l) for l in sys.stdin]; print('train', [(d['step'], d['loss']) for d in r][::3], 'tok/s', r[-1]['tok_per_s_node'])"
 fi
+if [ -n "$M350" ]; then  # BASELINE cfg 4's model through FSDP on one forced-RCCL rank: resident and FULL_SHARD-resharded
+  run m350_fsdp 400 env GPT2MI_FORCE_COLLECTIVES=1 $TR bench.py --no-cpu-baseline --parallel fsdp --model 350M \
+    --batch 32 || exit $?
+  run m350_fsdp_reshard 400 env GPT2MI_FORCE_COLLECTIVES=1 $TR bench.py --no-cpu-baseline --parallel fsdp --reshard \
+    --model 350M --batch 32 || exit $?
+fi
