@@ -64,3 +64,14 @@ if [ -n "$M350" ]; then  # BASELINE cfg 4's model through FSDP on one forced-RCC
   run m350_fsdp_reshard 400 env GPT2MI_FORCE_COLLECTIVES=1 $TR bench.py --no-cpu-baseline --parallel fsdp --reshard \
     --model 350M --batch 32 || exit $?
 fi
+if [ -n "$PROFW" ]; then  # rocprof of the one-rank wrapped lines (forced RCCL collectives): where the wrapper's time goes
+  for v in "ddp:--parallel ddp" "fsdp:--parallel fsdp" "fsdprs:--parallel fsdp --reshard"; do
+    name=${v%%:*}; args=${v#*:}
+    timeout -k 10 300 env GPT2MI_FORCE_COLLECTIVES=1 WORLD_SIZE=1 RANK=0 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 \
+      MASTER_PORT=29591 rocprofv3 --kernel-trace --stats -d $O/prof_$name -o run -- python bench.py --steps 5 \
+      --warmup 3 --no-cpu-baseline $args > $O/prof_$name.log 2>&1 || exit $?
+    python tools/rocpd_stats.py $O/prof_$name/run_results.db $O/kernel_stats_$name.csv && \
+      python tools/prof_summary.py $O/kernel_stats_$name.csv 8 > $O/summary_$name.txt 2>&1
+    echo "== $name"; head -8 $O/summary_$name.txt; tail -1 $O/summary_$name.txt
+  done
+fi
