@@ -107,7 +107,8 @@ res = {}
 for variant in os.environ["VARIANTS"].split(","):
     mode, kind, prec = variant.split("/")
     opt_kind = "torch" if kind in ("torch", "rstorch") else "fused"
-    m, wrap, opt = build(mode, opt_kind, overlap=kind == "overlap", reshard=kind in ("reshard", "ckptrs", "rstorch"))
+    m, wrap, opt = build(mode, opt_kind, overlap=kind in ("overlap", "rsoverlap"),
+                         reshard=kind in ("reshard", "ckptrs", "rstorch", "rsoverlap"))
     losses, norms = [], []
     if kind in ("ckpt", "ckptrs", "ckptx"):  # ckptrs: saved and resumed resharded; ckptx: resident -> resharded
         step(wrap, opt, 0, prec, opt_kind, False)
@@ -135,7 +136,7 @@ dist.barrier(); dist.destroy_process_group()
 VARIANTS = ["ddp/fused/fp32", "ddp/fused/bf16", "ddp/overlap/fp32", "ddp/torch/fp32", "ddp/nosync/fp32",
             "fsdp/overlap/fp32", "fsdp/fused/fp32",
             "fsdp/fused/bf16", "fsdp/torch/fp32", "fsdp/ckpt/bf16", "ddp/ckpt/fp32", "fsdp/reshard/fp32",
-            "fsdp/reshard/bf16", "fsdp/ckptrs/bf16", "fsdp/ckptx/fp32", "fsdp/rstorch/fp32"]
+            "fsdp/reshard/bf16", "fsdp/ckptrs/bf16", "fsdp/ckptx/fp32", "fsdp/rstorch/fp32", "fsdp/rsoverlap/bf16"]
 
 
 def _launch(tmp, nproc, variants, port, golden="ddp_golden.json", **env_extra):
@@ -159,7 +160,7 @@ def results(tmp_path_factory):
 
 
 RCCL_VARIANTS = ["ddp/fused/fp32", "ddp/fused/bf16", "ddp/overlap/bf16", "ddp/torch/fp32", "fsdp/fused/fp32",
-                 "fsdp/fused/bf16", "fsdp/overlap/bf16", "fsdp/reshard/bf16"]
+                 "fsdp/fused/bf16", "fsdp/overlap/bf16", "fsdp/reshard/bf16", "fsdp/rsoverlap/bf16"]
 
 
 @pytest.fixture(scope="module")
