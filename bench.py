@@ -29,7 +29,10 @@ import os
 import sys
 import time
 
-import torch
+# kernel arguments in device memory (set before the HIP runtime starts; see gpt_2_distributed_amd/__init__.py)
+os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
+
+import torch  # noqa: E402
 import torch.distributed as dist
 
 PEAK_BF16_TFLOPS = 256 * 4 * 1024 * 2.4e9 / 1e12  # 2516.6 dense bf16 (MI355X_MICROARCH.md)
