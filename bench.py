@@ -29,7 +29,8 @@ import os
 import sys
 import time
 
-# kernel arguments in device memory (set before the HIP runtime starts; see gpt_2_distributed_amd/__init__.py)
+# kernel arguments in device memory (set before the HIP runtime starts; an entry-point setting, see
+# gpt_2_distributed_amd/__init__.py and INTEGRATION.md §4)
 os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
 
 import torch  # noqa: E402
@@ -88,8 +89,10 @@ def main():
     # optimizer step over grad_accum micro-batches of --batch sequences per rank
     ap.add_argument("--parallel", choices=["ddp", "fsdp"], default="ddp", help="multi-rank wrapper (N > 1)")
     ap.add_argument("--grad_accum", type=int, default=1)
-    ap.add_argument("--reshard", action="store_true",
-                    help="--parallel fsdp: reshard_after_forward (FULL_SHARD's memory behaviour; default: resident units)")
+    ap.add_argument("--resident", action="store_true",
+                    help="--parallel fsdp: keep gathered units resident (default: reshard after forward, FULL_SHARD's "
+                         "memory behaviour as in the reference)")
+    ap.add_argument("--reshard", action="store_true", help="--parallel fsdp: the default (kept for older scripts)")
     ap.add_argument("--probe-every", type=int, default=5,
                     help="time the probed kernel launches (HIP events) in every N-th timed step")
     args = ap.parse_args()
@@ -114,7 +117,7 @@ def main():
         from gpt_2_distributed_amd.parallel import DistributedDataParallel, ShardedDataParallel
         wrap = ShardedDataParallel if args.parallel == "fsdp" else DistributedDataParallel
         # the embeddings' all-reduce (DDP) / reduce-scatter (FSDP) runs under the optimizer step of every other range
-        extra = dict(reshard_after_forward=True) if args.parallel == "fsdp" and args.reshard else {}
+        extra = dict(reshard_after_forward=not args.resident) if args.parallel == "fsdp" else {}
         ddp = wrap(model, bucket_mb=args.bucket_mb, overlap_optimizer=True, **extra)
         opt = ddp.configure_optimizers(learning_rate=1e-4)
         fwd = ddp
@@ -136,7 +139,7 @@ def main():
         # the reference loop (:400-425) runs every micro-step's backward synced; the resident wrappers skip the
         # collective on all but the last one (no_sync: the same sums), the resharded FSDP reduce-scatters every one
         # as the reference does (its gradients do not outlive their unit's backward)
-        sync_each = args.parallel == "fsdp" and args.reshard
+        sync_each = args.parallel == "fsdp" and not args.resident
         for a in range(GA):
             x, y = batches[(i * GA + a) % len(batches)]
             ctx = fwd.no_sync() if (a + 1 < GA and hasattr(fwd, "no_sync") and not sync_each) \
@@ -236,7 +239,7 @@ def main():
         "config": {"workload": f"GPT-2 {args.model} training step: fwd+loss+bwd+AdamW"
                                + ({"ddp": " + bucketed grad all-reduce in the backward",
                                    "fsdp": " + per-block FSDP all-gather / reduce-scatter"
-                                   + (", resharded after forward" if args.reshard else "")}[args.parallel]
+                                   + (", resident units" if args.resident else ", resharded after forward")}[args.parallel]
                                   if wrapped else "")
                                + f", dropout {args.dropout}" + (f", {GA} accumulated micro-batches" if GA > 1 else ""),
                    "model": f"GPT-2 {args.model}", "global_batch": B * world * GA, "seq_len": T,

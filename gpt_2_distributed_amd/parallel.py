@@ -24,9 +24,12 @@ Replaces the reference's ``DDP(model, device_ids=[device])`` / ``FSDP(model, ...
   stream, as many as fit a byte budget of gathered output (``prefetch_bytes``, like FSDP's ``limit_all_gathers``
   rate limiter; ``prefetch_depth`` caps it by a unit count). In the backward each unit's gradient range is reduce-scattered (bf16
   under autocast, like reduce_dtype=bf16) the moment the engine marks it final, overlapped with the
-  remaining backward. MI355X-first difference: a gathered unit stays resident until the next optimizer
-  step (288 GB HBM holds every unit of every BASELINE model), so the backward does not re-gather it and
-  gradient-accumulation micro-steps gather once per optimizer step; the math is FULL_SHARD's.
+  remaining backward. By default (``reshard_after_forward=True``, torch FSDP's FULL_SHARD default, which the
+  reference runs) each block unit's gathered parameters are released after its forward and gathered again for
+  its backward, so per-rank memory falls with the world size. ``reshard_after_forward=False`` is the MI355X
+  resident mode: a gathered unit stays until the next optimizer step (288 GB HBM holds every unit of every
+  BASELINE model), so the backward does not re-gather it and gradient-accumulation micro-steps gather once per
+  optimizer step; the math is FULL_SHARD's either way.
 
 Gradient scaling: every collective is a SUM. A synced backward computes its gradients pre-divided by
 world (``GradHooks.begin_backward``); gradients accumulated earlier (no_sync micro-steps, or an
@@ -367,7 +370,9 @@ def fsdp_memory_plan(units, world: int, reshard: bool) -> dict:
     total = units[-1][2]
     if not reshard:
         views = total * (4 + 2 + 2 + 4)
-        staging = sum(p.per * world for p in plans) * (2 + 2)
+        # each unit's bf16 gather buffer less this rank's chunk of it (the bf16 shard, in the sharded state) + its bf16
+        # reduce-scatter input
+        staging = sum(p.per * (world - 1) * 2 + p.per * world * 2 for p in plans)
     else:
         root = [p for p in plans if p.name in ("embed", "head")]
         blocks = [p for p in plans if p.name not in ("embed", "head")]
@@ -375,8 +380,10 @@ def fsdp_memory_plan(units, world: int, reshard: bool) -> dict:
         per_b = max((p.per for p in blocks), default=0)
         views = sum(p.n for p in root) * (4 + 2 + 2 + 4) + \
             _ReshardStore.P_SLOTS * nb * (4 + 2 + 2) + _ReshardStore.G_SLOTS * nb * 4
+        # the block gather and reduce-scatter rings, the root's own gather and reduce-scatter buffers, and each block's
+        # reduced bf16 shard (the bf16 shard itself is in the sharded state)
         staging = 2 * FullyShardedDataParallel.STAGE_SLOTS * per_b * world * 2 + \
-            sum(p.per * world for p in root) * (2 + 2) + shard_total * 2
+            sum(p.per * world for p in root) * (2 + 2) + sum(p.per for p in blocks) * 2
     return {"sharded_state_bytes": sharded, "compute_view_bytes": views, "staging_bytes": staging,
             "total": sharded + views + staging}
 
@@ -522,14 +529,14 @@ class FullyShardedDataParallel(nn.Module):
 
     def __init__(self, module, device_ids=None, bucket_mb: float = 64.0, prefetch: bool = True,
                  prefetch_depth: Optional[int] = None, overlap_optimizer: bool = False,
-                 prefetch_bytes: Optional[int] = None, reshard_after_forward: bool = False):
+                 prefetch_bytes: Optional[int] = None, reshard_after_forward: bool = True):
         super().__init__()
         self.module = module
         # reshard_after_forward: FULL_SHARD's memory behaviour (torch FSDP's default for FULL_SHARD, which the
-        # reference runs, train_gpt2_distributed.py:146-161): a GPT2Block unit's gathered parameters are released
-        # after its forward and gathered again for its backward, its gradient lives only until its reduce-scatter, and
-        # the full-model compute views are freed (_ReshardStore). Off (default): every gathered unit stays resident
-        # until the next optimizer step (no re-gather: 288 GB holds every BASELINE model's views).
+        # reference runs, train_gpt2_distributed.py:146-161; the default here too): a GPT2Block unit's gathered
+        # parameters are released after its forward and gathered again for its backward, its gradient lives only until
+        # its reduce-scatter, and the full-model compute views are freed (_ReshardStore). Off: every gathered unit stays
+        # resident until the next optimizer step (no re-gather: 288 GB holds every BASELINE model's views).
         self.reshard_after_forward = bool(reshard_after_forward)
         self.store: Optional[_ReshardStore] = None
         # overlap_optimizer (with configure_optimizers' ShardedAdamW): the backward returns with the last unit's
@@ -594,7 +601,12 @@ class FullyShardedDataParallel(nn.Module):
             self.store.evicted = self._evicted
             eng.store = self.store
             # the full-model views are freed (as FSDP frees the unsharded FlatParameter): the module's own parameters
-            # keep their shapes but no storage; every view the engine forms comes from the store
+            # keep their shapes but no storage; every view the engine forms comes from the store. Their .grad views
+            # pointed into the freed grad arena, so they are dropped: the inner module's parameters then read as
+            # torch FSDP's do after resharding (no gradient; data without storage), and what a caller uses is the
+            # wrapper's flat_param / state_dict()
+            for prm in eng.params_by_name.values():
+                prm.grad = None
             for t in (module.arena, eng.shadow, eng.shadowT, eng.grad):
                 t.untyped_storage().resize_(0)
 
@@ -614,11 +626,22 @@ class FullyShardedDataParallel(nn.Module):
         n_full = self.module.layout.total
         rs = self.store is not None
         views = self.store.view_bytes() if rs else n_full * (4 + 2 + 2 + 4)
+        # staging: every collective buffer except the bf16 shard, which sharded_state_bytes counts (18 B/element): the
+        # resharded mode's "shard16" buffer, or in the resident mode this rank's chunk of each bf16 gather buffer
+        staging = 0
+        for (kind, unit, dtype), t in self._bufs.items():
+            if kind == "shard16":
+                continue
+            n = t.numel()
+            if kind == "ag" and dtype == torch.bfloat16 and not rs:
+                n -= self.plan[unit].per
+            staging += n * t.element_size()
         return {"params": n_full, "world": self.world, "reshard_after_forward": rs,
                 "sharded_state_bytes": self.shard_total * (4 + 4 + 8 + 2),
                 "ddp_equivalent_state_bytes": n_full * (4 + 4 + 8),
                 "compute_view_bytes": views,
-                "staging_bytes": sum(t.numel() * t.element_size() for t in self._bufs.values()),
+                "staging_bytes": staging,
+                "plan": fsdp_memory_plan(self.units, self.world, rs),  # the same rank priced (activations excluded)
                 "per_rank_bytes_by_world": {w: fsdp_memory_plan(self.units, w, rs)["total"] for w in (1, 2, 4, 8)}}
 
     # ---- buffers ------------------------------------------------------------------------------------
@@ -667,8 +690,18 @@ class FullyShardedDataParallel(nn.Module):
     STAGE_SLOTS = 3
 
     def _ring(self, ring, dtype, n):
-        """The next slot of staging ring ``ring`` (STAGE_SLOTS buffers of n elements): (index, buffer)."""
+        """The next slot of staging ring ``ring`` (STAGE_SLOTS buffers of n elements): (index, buffer). A gather
+        ring's slot is handed out only when the unit it holds has been unpacked (no longer pending), a reduce-scatter
+        ring's only when the reduce-scatter that read it has been waited for: refilling it earlier would overwrite
+        bytes a collective or the unpack still reads (the ordering argument is in stream order: ProcessGroupNCCL makes
+        the collective's stream wait on the current stream at issue, and the compute stream waits on the collective
+        before it reads the slot)."""
         i = self._stage_next.get(ring, 0)
+        if self._stage_user.get((ring, i)) in self._pending:
+            raise RuntimeError(f"FSDP staging ring {ring}: slot {i} still holds the pending gather of "
+                               f"{self._stage_user[(ring, i)]}")
+        if (ring, i) in self._rs_slot_work:
+            raise RuntimeError(f"FSDP staging ring {ring}: slot {i} is still read by an unwaited reduce-scatter")
         self._stage_next[ring] = (i + 1) % self.STAGE_SLOTS
         return i, self._buf(ring, i, dtype, n)
 
@@ -764,7 +797,7 @@ class FullyShardedDataParallel(nn.Module):
 
     def _gather_bytes(self, unit, dtype) -> int:
         p = self.plan[unit]
-        return p.per * self.world * torch.empty((), dtype=dtype).element_size()
+        return p.per * self.world * dtype.itemsize
 
     def _prefetch_after(self, unit, dtype, backward=False):
         """Issue the all-gathers of the units after ``unit`` (forward order; backward order for a backward re-gather)
@@ -815,11 +848,11 @@ class FullyShardedDataParallel(nn.Module):
             # reshard_after_forward: the packed input goes to a staging ring (its slot's previous reduce-scatter waited
             # for first), the reduced shard to a shard-sized buffer of the unit; the gradient slot is free once packed
             ring = "rs16" if dtype == torch.bfloat16 else "rs32"
+            prev = self._rs_slot_work.pop((ring, self._stage_next.get(ring, 0)), None)
+            if prev is not None:  # the slot's previous reduce-scatter completes before the pack below refills it
+                prev.wait()
             i, inp = self._ring(ring, dtype, self._block_ag_len())
             inp = inp[:n]
-            prev = self._rs_slot_work.pop((ring, i), None)
-            if prev is not None:
-                prev.wait()
             slot = (ring, i)
             out = self._buf("rs_out", unit, dtype, p.per)
             K.fsdp_pack(self.store.unit_grad(unit), inp, p.n, n)

@@ -61,9 +61,15 @@ def build_parser():
     p.add_argument("--synthetic_tokens", type=int, default=2_000_000)
     p.add_argument("--resume", type=str, default="", help="checkpoint step_XXXXXXX directory to resume from")
     p.add_argument("--log_every", type=int, default=20)
+    # fsdp memory behaviour: the reference's FSDP(sharding_strategy=FULL_SHARD) (train_gpt2_distributed.py:156-161)
+    # frees each block's gathered parameters after its forward and gathers them again for its backward; that is the
+    # default here too. --fsdp_resident keeps every gathered unit until the optimizer step instead (no re-gather in
+    # the backward; per-rank memory then does not shrink with the world size: DESIGN.md §5)
+    p.add_argument("--fsdp_resident", action="store_true",
+                   help="fsdp: keep each gathered unit resident until the optimizer step instead of FULL_SHARD's "
+                        "reshard after forward")
     p.add_argument("--fsdp_reshard", action="store_true",
-                   help="fsdp: release each block's gathered parameters after its forward (FULL_SHARD's memory "
-                        "behaviour) instead of keeping them resident until the optimizer step")
+                   help="fsdp: reshard after forward (the default; kept for command lines of earlier rounds)")
     return p
 
 
@@ -183,7 +189,7 @@ def main(argv=None):
     if args.training_mode == "ddp":
         model = DistributedDataParallel(base, overlap_optimizer=True)  # the grad norm comes from the fused AdamW
     elif args.training_mode == "fsdp":
-        model = FullyShardedDataParallel(base, overlap_optimizer=True, reshard_after_forward=args.fsdp_reshard)
+        model = FullyShardedDataParallel(base, overlap_optimizer=True, reshard_after_forward=not args.fsdp_resident)
     else:
         model = base
     optim = model.configure_optimizers(weight_decay=0.1, learning_rate=args.lr, betas=(0.9, 0.95))
@@ -281,4 +287,7 @@ class _Null:
 
 
 if __name__ == "__main__":
+    # kernel arguments in device memory (gpt_2_distributed_amd/__init__.py); read when the HIP runtime starts, which
+    # has not happened yet (importing torch does not start it); an explicit setting in the environment wins
+    os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
     main()

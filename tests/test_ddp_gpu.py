@@ -128,6 +128,10 @@ for variant in os.environ["VARIANTS"].split(","):
     res[variant] = {"losses": losses, "norms": norms, "params": fp}
     if mode == "fsdp":
         res[variant]["mem"] = wrap.memory_report()
+        # resharded: the inner module's parameters expose no gradient (their views were freed with the grad arena;
+        # ADVICE r5), as torch FSDP's after resharding; the wrapper's flat_param carries the shard's gradient
+        res[variant]["inner_grads_none"] = all(p.grad is None for p in m.parameters()) if wrap.store is not None \
+            else None
 if r == 0:
     print("RESULT", json.dumps(res), flush=True)
 dist.barrier(); dist.destroy_process_group()
@@ -213,15 +217,23 @@ def test_rccl_collectives_vs_reference(rccl_results, variant):
     _check_vs_golden(rccl_results[variant], variant)
 
 
+def test_resharded_inner_parameters_expose_no_gradient(results):
+    for v in ("fsdp/reshard/bf16", "fsdp/reshard/fp32"):
+        if v in results:
+            assert results[v]["inner_grads_none"] is True, v
+
+
 WIDE = {name: json.load(open(os.path.join(GOLDEN, name)))
         for name in ("cfg5_golden.json", "cfg4_golden.json", "ddp124_golden.json")}
 WIDE_RUNS = {  # (golden file, ranks, backend, variants, extra env)
     "cfg5_gloo2": ("cfg5_golden.json", 2, "gloo", ["fsdp/fused/fp32", "fsdp/fused/bf16", "fsdp/torch/fp32",
                                                     "fsdp/reshard/fp32", "fsdp/reshard/bf16"], {}),
-    "cfg5_rccl1": ("cfg5_golden.json", 1, "nccl", ["fsdp/fused/fp32", "fsdp/fused/bf16"], {}),
+    "cfg5_rccl1": ("cfg5_golden.json", 1, "nccl", ["fsdp/fused/fp32", "fsdp/fused/bf16", "fsdp/reshard/fp32",
+                                                    "fsdp/reshard/bf16"], {}),
     "cfg4_gloo2": ("cfg4_golden.json", 2, "gloo", ["fsdp/fused/fp32", "fsdp/fused/bf16", "fsdp/overlap/bf16",
                                                     "fsdp/torch/fp32", "fsdp/reshard/fp32", "fsdp/reshard/bf16"], {}),
-    "cfg4_rccl1": ("cfg4_golden.json", 1, "nccl", ["fsdp/fused/fp32", "fsdp/fused/bf16", "fsdp/overlap/bf16"], {}),
+    "cfg4_rccl1": ("cfg4_golden.json", 1, "nccl", ["fsdp/fused/fp32", "fsdp/fused/bf16", "fsdp/overlap/bf16",
+                                                    "fsdp/reshard/fp32", "fsdp/reshard/bf16"], {}),
     "ddp124_gloo2": ("ddp124_golden.json", 2, "gloo", ["ddp/fused/fp32", "ddp/fused/bf16", "ddp/overlap/bf16",
                                                         "ddp/torch/fp32"], {"BUCKET_MB": "25"}),
     "ddp124_rccl1": ("ddp124_golden.json", 1, "nccl", ["ddp/fused/bf16", "ddp/overlap/bf16"], {"BUCKET_MB": "25"}),
@@ -301,4 +313,13 @@ def test_fsdp_reshard_memory_report(results, wide_results):
         assert rs["sharded_state_bytes"] == rd["sharded_state_bytes"]
         w = {int(k): v for k, v in rs["per_rank_bytes_by_world"].items()}
         assert w[1] > w[2] > w[4] > w[8]
-        assert _ReshardStore.P_SLOTS == 2 and _ReshardStore.G_SLOTS == 3
+        # the live wrappers allocate what fsdp_memory_plan prices at their world size: the same sharded
+        # state and compute views; staging up to the plan (a staging ring slot is allocated at its first use, so a
+        # short run may not have touched all of them), the bf16 shard counted once, in the sharded state
+        for live in (rs, rd):
+            plan = live["plan"]
+            assert live["sharded_state_bytes"] == plan["sharded_state_bytes"], live
+            assert live["compute_view_bytes"] == plan["compute_view_bytes"], live
+            assert live["staging_bytes"] <= plan["staging_bytes"], live
+        assert rd["staging_bytes"] == rd["plan"]["staging_bytes"], rd  # resident: every unit's buffers exist
+        assert rs["compute_view_bytes"] < rd["compute_view_bytes"]

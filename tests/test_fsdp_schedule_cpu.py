@@ -123,3 +123,50 @@ def test_reshard_memory_plan_of_the_baseline_models():
         assert v8 == fsdp_memory_plan(units, 1, True)["compute_view_bytes"]  # independent of the world size
         print(name, "per-rank GB at 1/2/4/8 ranks: reshard", [round(x / 1e9, 2) for x in rs],
               "resident", [round(x / 1e9, 2) for x in rd])
+
+
+def test_staging_ring_slots_are_not_reissued_while_in_use():
+    """reshard_after_forward's 3-slot staging rings. A gather ring's next slot is not handed out while the
+    unit it holds is still pending (not unpacked), nor a reduce-scatter ring's while the reduce-scatter that read it
+    has not been waited for; the ring otherwise walks its slots round-robin."""
+    import pytest
+    bf = torch.bfloat16
+    f, _ = _stand_in()
+    f.flat_param = nn.Parameter(torch.zeros(4))
+    f._bufs, f._stage_next, f._stage_user, f._rs_slot_work = {}, {}, {}, {}
+    S = FullyShardedDataParallel.STAGE_SLOTS
+    for k in range(S):  # three gathers in flight, one per slot
+        i, _buf = f._ring("ag16", bf, 8)
+        assert i == k
+        f._stage_user[("ag16", i)] = f"h.{k}"
+        f._pending[f"h.{k}"] = (_Work(), bf, None)
+    assert not f._ring_free("ag16")
+    with pytest.raises(RuntimeError, match="pending gather of h.0"):
+        f._ring("ag16", bf, 8)
+    f._pending.pop("h.0")  # h.0 unpacked: its slot may be refilled
+    assert f._ring_free("ag16") and f._ring("ag16", bf, 8)[0] == 0
+    # reduce-scatter ring: a slot whose reduce-scatter was not waited for is refused
+    w = _Work()
+    i, _buf = f._ring("rs16", bf, 8)
+    f._rs_slot_work[("rs16", i)] = w
+    for _ in range(S - 1):
+        f._ring("rs16", bf, 8)
+    with pytest.raises(RuntimeError, match="unwaited reduce-scatter"):
+        f._ring("rs16", bf, 8)
+    f._rs_slot_work.pop(("rs16", i)).wait()
+    assert f._ring("rs16", bf, 8)[0] == i and w.waited
+
+
+def test_memory_plan_counts_the_bf16_shard_once():
+    """the bf16 shard is part of the sharded state (18 B per sharded element); the staging the plan prices
+    leaves it out in both modes (resident: this rank's chunk of every unit's bf16 gather buffer; resharded: the shard
+    buffer), so at one rank the resident mode stages only the reduce-scatter inputs."""
+    from gpt_2_distributed_amd.parallel import fsdp_memory_plan, plan_shards
+    units = _units(dict(n_embd=768, n_layer=12, vocab_size=50257))
+    plans, shard_total = plan_shards(units, 1)
+    rd = fsdp_memory_plan(units, 1, False)
+    assert rd["staging_bytes"] == shard_total * 2  # world 1: gather buffer == shard; one bf16 reduce-scatter input
+    plans8, shard8 = plan_shards(units, 8)
+    rd8 = fsdp_memory_plan(units, 8, False)
+    assert rd8["staging_bytes"] == sum(p.per * 7 * 2 + p.per * 8 * 2 for p in plans8)
+    assert rd8["sharded_state_bytes"] == shard8 * 18

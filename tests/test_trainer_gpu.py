@@ -158,15 +158,15 @@ def test_trainer_cli_end_to_end(tmp_path):
         assert (ckpt / st / "model.pt").exists() and (ckpt / st / "optim.pt").exists()
 
 
-@pytest.mark.parametrize("mode", ["ddp", "fsdp", "fsdp_reshard"])
+@pytest.mark.parametrize("mode", ["ddp", "fsdp", "fsdp_resident"])
 def test_trainer_cli_wrapped_one_rank_resume(tmp_path, mode):
-    """The trainer under torchrun in the reference's ddp / fsdp modes (one rank, RCCL collectives forced on), with
-    --fsdp_reshard (FULL_SHARD's memory behaviour: every micro-step reduce-scatters, no no_sync), 2 micro-batches
-    per step: 2 steps + a resume for 2 more log the losses of 4 uninterrupted steps (the sharded checkpoint:
-    model.pt gathered on rank 0, optim_rank{r}.pt per rank)."""
+    """The trainer under torchrun in the reference's ddp / fsdp modes (one rank, RCCL collectives forced on); fsdp is
+    FULL_SHARD's memory behaviour by default, as the reference's (every micro-step reduce-scatters, no no_sync), and
+    --fsdp_resident keeps the gathered units; 2 micro-batches per step: 2 steps + a resume for 2 more log the losses
+    of 4 uninterrupted steps (the sharded checkpoint: model.pt gathered on rank 0, optim_rank{r}.pt per rank)."""
     data = tmp_path / "data"
-    mode_args = ["--training_mode", "fsdp", "--fsdp_reshard"] if mode == "fsdp_reshard" else ["--training_mode", mode]
-    port = {"ddp": 29571, "fsdp": 29572, "fsdp_reshard": 29573}[mode]
+    mode_args = ["--training_mode", "fsdp", "--fsdp_resident"] if mode == "fsdp_resident" else ["--training_mode", mode]
+    port = {"ddp": 29571, "fsdp": 29572, "fsdp_resident": 29573}[mode]
     base = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1", "--master-addr=127.0.0.1",
             f"--master-port={port}", "-m", "gpt_2_distributed_amd.train_gpt2_distributed", "--data_dir", str(data),
             "--synthetic", "2", "--synthetic_tokens", "60000", "--seq_len", "128", "--batch", "4", "--model", "124M",
