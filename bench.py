@@ -184,9 +184,11 @@ def main():
     kflops = {
         "lm_head_fwd": 2.0 * M * V * C, "lm_head_dgrad": 2.0 * M * V * C, "lm_head_wgrad": 2.0 * M * V * C,
         "fc1_fwd": 2.0 * M * 4 * C * C, "attn_fwd": 4.0 * B * H * (T * (T + 1) / 2) * (C // H),
-        # the weight-gradient family (one kernel, 1 + 4L launches a step: tied lm_head + qkv / proj / fc1 / fc2 of
-        # every block, each with its split-K reduction): the average algorithmic FLOPs of a launch
-        "wgrad": (2.0 * M * V * C + cfg.n_layer * 2.0 * M * 12 * C * C) / (1 + 4 * cfg.n_layer),
+        # the weight-gradient family (the tied lm_head + every block's qkv / proj / fc1 / fc2 weight gradients, each
+        # launch with its split-K reduction; 1 + L launches a step since round 6, a block's four grouped in one, 1 + 4L
+        # before): the average algorithmic FLOPs of a launch = the step's weight-gradient FLOPs / its launches
+        "wgrad": (2.0 * M * V * C + cfg.n_layer * 2.0 * M * 12 * C * C)
+        / max(1.0, len(armed["wgrad"]) / len(range(0, args.steps, every))),
     }
     kernels = {}
     for name, evs in armed.items():

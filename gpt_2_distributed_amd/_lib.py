@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("GPT2MI_LIB") or os.path.join(_HERE, "libgpt2mi.so")
 
 # the ABI these bindings are written against (include/gpt2mi.h GPT2MI_ABI_VERSION): a stale or foreign
 # library is refused at load instead of being called with the wrong argument lists
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 _c_int, _c_float, _c_size, _c_u64, _p = ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_void_p
 
@@ -68,6 +68,10 @@ _SIGS = {
                           _c_size, _c_int, _c_int, _p],
     "gpt2mi_gemm_wgrad_kt": [_c_int, _c_int, _c_int, _p, _c_int, _p, _c_int, _p, _c_int, _c_int, _c_float, _p, _p,
                              _c_size, _c_int, _c_int, _p],
+    # count, M[], N[], K, A[], lda[], B[], ldb[], C[] (host arrays), accumulate, alpha, alpha_dev, ws, ws_floats, splits,
+    # sched, stream
+    "gpt2mi_gemm_wgrad_grouped": [_c_int, _p, _p, _c_int, _p, _p, _p, _p, _p, _c_int, _c_float, _p, _p, _c_size,
+                                  _c_int, _c_int, _p],
 }
 _RESTYPES = {"gpt2mi_last_error": ctypes.c_char_p}
 
@@ -193,6 +197,37 @@ def gemm_wgrad_kt(M, N, K, A, lda, Bt, ldbt, C, ldc, accumulate=True, alpha=1.0,
     ws_n = workspace.numel() if workspace is not None else 0
     _call("gpt2mi_gemm_wgrad_kt", M, N, K, _ptr(A), lda, _ptr(Bt), ldbt, _ptr(C), ldc, int(accumulate), alpha,
           _ptr(alpha_dev), _ptr(workspace), ws_n, splits, int(sched), _stream())
+
+
+def gemm_wgrad_grouped(problems, K, accumulate=True, alpha=1.0, alpha_dev=None, workspace=None, splits=1,
+                       sched=SCHED_AUTO):
+    """Up to 4 weight gradients over the same K tokens in one launch (+ one reduction): problems = [(M, N, A, lda, B,
+    ldb, C)], each C[M][N] (+)= alpha A^T B as gemm_wgrad with the same splits and fp32 slabs would form it."""
+    n = len(problems)
+    ints = lambda vals: (_c_int * n)(*vals)  # noqa: E731
+    ptrs = lambda vals: (_p * n)(*vals)  # noqa: E731
+    ws_n = workspace.numel() if workspace is not None else 0
+    _call("gpt2mi_gemm_wgrad_grouped", n, ints([q[0] for q in problems]), ints([q[1] for q in problems]), K,
+          ptrs([_ptr(q[2]) for q in problems]), ints([q[3] for q in problems]), ptrs([_ptr(q[4]) for q in problems]),
+          ints([q[5] for q in problems]), ptrs([_ptr(q[6]) for q in problems]), int(accumulate), alpha,
+          _ptr(alpha_dev), _ptr(workspace), ws_n, splits, int(sched), _stream())
+
+
+def wgrad_group_splits(shapes, K, cus=256):
+    """Split-K factor of a grouped weight-gradient launch over output shapes [(M, N)] (256-multiples): the
+    wgrad_splits cost model on the summed tile count, so that the last round of blocks is not mostly idle (a GPT2Block
+    of GPT-2 124M: 108 tiles x 7 splits = 756 blocks, 2.95 rounds of 256)."""
+    tiles = sum((m // 256) * (n // 256) for m, n in shapes)
+    elems = sum(m * n for m, n in shapes)
+    best, best_cost = 1, None
+    for s in range(1, 33):
+        if K // s < 256:
+            break
+        rounds = -(-tiles * s // cus)
+        cost = rounds * (K / s) * 22e-9 + (s * elems * 8 / 5e12 if s > 1 else 0.0)
+        if best_cost is None or cost < best_cost * 0.99:
+            best, best_cost = s, cost
+    return best
 
 
 def wgrad_splits(M, N, K, cus=256):

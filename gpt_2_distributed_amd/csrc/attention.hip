@@ -39,6 +39,13 @@ constexpr int BKV = 64;  // keys per K/V tile in fwd / dQ
 GPT2MI_PRODUCT_KNOB(ATTN_FWD_OCC, 3);
 GPT2MI_PRODUCT_KNOB(ATTN_FWD_LMAX, 1);
 constexpr int BKB = 128;  // keys per workgroup in dK/dV (4 waves of 32)
+#ifndef ATTN_DKDV_PIPE
+#define ATTN_DKDV_PIPE 0  // dK/dV tile body: 0 phases in separate blocks; 1-3 one block per DIAG variant (A/B builds)
+#endif
+#ifndef ATTN_DKDV_FILL
+#define ATTN_DKDV_FILL 10  // ATTN_DKDV_PIPE 3: VALU instructions placed after each MFMA
+#endif
+GPT2MI_PRODUCT_KNOB(ATTN_DKDV_PIPE, 0);
 constexpr int kThreads = 256;
 constexpr float kLog2e = 1.4426950408889634f;
 
@@ -565,7 +572,11 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkdv_kernel(const bf16* __res
   const int C = H * D;
   const size_t ld = 3 * (size_t)C;
   const bf16* base = qkv + (size_t)b * T * ld;
+#if ATTN_DKDV_PIPE == 0
   const int k_lo = kb * 128 + 32 * w;
+#else
+  const int k_lo = kb * 128 + 32 * __builtin_amdgcn_readfirstlane(w);  // wave-uniform: scalar branches on it
+#endif
   const bool wave_valid = k_lo < T;
   // K and V rows kb*128 .. +128 (clamped to T - 1 past the end: only invalid waves read those) into LDS, swizzled as
   // every tile (t_off); 4 chunks of 16 B per thread and array
@@ -617,101 +628,240 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkdv_kernel(const bf16* __res
   __syncthreads();
   const char* Kw = Kl + 32 * w * 128;  // this wave's 32 keys
   const char* Vw = Vl + 32 * w * 128;
-  for (int i = i0; i < nqt; ++i) {
+  // one query tile: Q / dO / lse / delta of tile i are in stage (i - i0) & 1; the next tile is staged under it
+  auto step = [&](int i, auto work) {
     const int cur = (i - i0) & 1;
     const char* Qs = stg + cur * kStage;
     const char* Ds = Qs + kTile;
     const float* Ls = reinterpret_cast<const float*>(Qs + 2 * kTile);
     const float* Dl = Ls + BQ3;
     if (i + 1 < nqt) gload(i + 1, stg + (cur ^ 1) * kStage);
-    const int q0 = i * BQ3;
-    if (wave_valid && q0 + BQ3 - 1 >= k_lo) {
-      const bool diag = q0 < k_lo + 31;
-      const uint32_t pre_t = DROP ? drop_pre(seed32(seed), ((uint32_t)bh * T + q0 + 4 * g) * (uint32_t)T + k_lo + (lane & 15)) : 0u;
+    work(i * BQ3, Qs, Ds, Ls, Dl);
+    if (i + 1 < nqt) sstore(stg + (cur ^ 1) * kStage);
+    __syncthreads();
+  };
+  // the general tile: a wave may be inactive (its keys after the tile's queries) or on the causal diagonal
+  auto general = [&](const int q0, const char* Qs, const char* Ds, const float* Ls, const float* Dl) {
+      if (wave_valid && q0 + BQ3 - 1 >= k_lo) {
+        const bool diag = q0 < k_lo + 31;
+        const uint32_t pre_t = DROP ? drop_pre(seed32(seed), ((uint32_t)bh * T + q0 + 4 * g) * (uint32_t)T + k_lo + (lane & 15)) : 0u;
+        f32x4 s[2][2], dp[2][2];  // [kg][fl]: S[q = q0 + 16fl + 4g + r][key = k_lo + 16kg + (l&15)]
+        f32x4 nl4[2], nd4[2];  // -lse * log2(e), -delta of the tile's queries
+#pragma unroll
+        for (int fl = 0; fl < 2; ++fl) {
+          nl4[fl] = *reinterpret_cast<const f32x4*>(Ls + 16 * fl + 4 * g);
+          nd4[fl] = *reinterpret_cast<const f32x4*>(Dl + 16 * fl + 4 * g);
+          s[0][fl] = s[1][fl] = f32x4{0.f, 0.f, 0.f, 0.f};
+          dp[0][fl] = dp[1][fl] = nd4[fl];
+        }
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          bf16x8 kfr[2], vfr[2];
+#pragma unroll
+          for (int kg = 0; kg < 2; ++kg) {
+            kfr[kg] = row_frag(Kw, 16 * kg, kk, lane);
+            vfr[kg] = row_frag(Vw, 16 * kg, kk, lane);
+          }
+#pragma unroll
+          for (int fl = 0; fl < 2; ++fl) {
+            const bf16x8 qa = row_frag(Qs, 16 * fl, kk, lane);
+            const bf16x8 da = row_frag(Ds, 16 * fl, kk, lane);
+#pragma unroll
+            for (int kg = 0; kg < 2; ++kg) {
+              s[kg][fl] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kfr[kg], s[kg][fl], 0, 0, 0);
+              dp[kg][fl] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, vfr[kg], dp[kg][fl], 0, 0, 0);
+            }
+          }
+        }
+        auto elementwise = [&](auto diag_c) {
+          constexpr bool DIAG = decltype(diag_c)::value;
+#pragma unroll
+          for (int kg = 0; kg < 2; ++kg) {
+            const int key = k_lo + 16 * kg + (lane & 15);
+            // the scores' affine part in place, as packed FMA pairs (v_pk_fma_f32; no register beyond s): x = s * sl2 - lse
+#pragma unroll
+            for (int fl = 0; fl < 2; ++fl)
+#pragma unroll
+              for (int r = 0; r < 4; r += 2) {
+                const f32x2 t = __builtin_elementwise_fma(f32x2{s[kg][fl][r], s[kg][fl][r + 1]}, f32x2{sl2, sl2},
+                                                          f32x2{nl4[fl][r], nl4[fl][r + 1]});
+                s[kg][fl][r] = t[0];
+                s[kg][fl][r + 1] = t[1];
+              }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              uint32_t km[2] = {~0u, ~0u};
+              if constexpr (DROP) {
+                uint32_t pv = pre_t;
+                asm volatile("" : "+v"(pv));  // hashed here, not hoisted ahead of the tile (its masks would not fit)
+                drop_keep_masks(tk2, drop_fin(pv + ((uint32_t)r * (uint32_t)T + 16u * kg) * kDropC1, seed_kx(seed)),
+                                km[0], km[1]);
+              }
+#pragma unroll
+              for (int fl = 0; fl < 2; ++fl) {
+                float p = __builtin_amdgcn_exp2f(s[kg][fl][r]);
+                if constexpr (DIAG) p = (q0 + 16 * fl + 4 * g + r < key) ? 0.f : p;
+                float pdv = p, d = dp[kg][fl][r];
+                if constexpr (DROP) {
+                  pdv = __uint_as_float(km[fl] & __float_as_uint(p));
+                  d = sel_mask(km[fl], d, nd4[fl][r]);
+                }
+                dp[kg][fl][r] = pdv;
+                s[kg][fl][r] = p * d;
+              }
+            }
+          }
+        };
+        if (diag) elementwise(std::true_type{});
+        else elementwise(std::false_type{});
+        const bf16x8 p0 = pack_perm(dp[0], 0), p1 = pack_perm(dp[1], 0);
+        const bf16x8 s0 = pack_perm(s[0], 0), s1 = pack_perm(s[1], 0);
+#pragma unroll
+        for (int fd = 0; fd < 4; ++fd) {
+          const bf16x8 dot = tr_frag(Ds, 0, 16 * fd, lane);
+          const bf16x8 qt = tr_frag(Qs, 0, 16 * fd, lane);
+          dv[0][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dot, p0, dv[0][fd], 0, 0, 0);
+          dv[1][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dot, p1, dv[1][fd], 0, 0, 0);
+          dk[0][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qt, s0, dk[0][fd], 0, 0, 0);
+          dk[1][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qt, s1, dk[1][fd], 0, 0, 0);
+        }
+      }
+  };
+#if ATTN_DKDV_PIPE == 0
+  for (int i = i0; i < nqt; ++i) step(i, general);
+#else
+  // Tiles i0 .. i0 + 3 hold every wave's diagonal tile (wave w: i0 + w) and the inactive waves; from i0 + 4 on every
+  // wave of the workgroup is active and off the diagonal, and the tile is ONE basic block: the S / dP MFMAs, the
+  // elementwise chain and the dV / dK MFMAs scheduled together (key group kg = 0 finished first, its dS formed while
+  // kg = 1's S / dP MFMAs run, its dV / dK MFMAs issued beside kg = 1's elementwise). The Q / dO row fragments are
+  // read per key group (re-read for kg = 1: 8 more ds_read_b128 per tile) instead of held for both (32 VGPRs past
+  // the 3-waves / SIMD budget).
+  for (int i = i0; i < min(i0 + 4, nqt); ++i) step(i, general);
+  auto steady = [&](const int q0, const char* Qs, const char* Ds, const float* Ls, const float* Dl) {
+    const uint32_t pre_t = DROP ? drop_pre(seed32(seed), ((uint32_t)bh * T + q0 + 4 * g) * (uint32_t)T + k_lo + (lane & 15)) : 0u;
+    auto tile = [&]() {
+      constexpr bool DIAG = false;
       f32x4 s[2][2], dp[2][2];  // [kg][fl]: S[q = q0 + 16fl + 4g + r][key = k_lo + 16kg + (l&15)]
       f32x4 nl4[2], nd4[2];  // -lse * log2(e), -delta of the tile's queries
 #pragma unroll
       for (int fl = 0; fl < 2; ++fl) {
         nl4[fl] = *reinterpret_cast<const f32x4*>(Ls + 16 * fl + 4 * g);
         nd4[fl] = *reinterpret_cast<const f32x4*>(Dl + 16 * fl + 4 * g);
-        s[0][fl] = s[1][fl] = f32x4{0.f, 0.f, 0.f, 0.f};
-        dp[0][fl] = dp[1][fl] = nd4[fl];
       }
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        bf16x8 kfr[2], vfr[2];
-#pragma unroll
-        for (int kg = 0; kg < 2; ++kg) {
-          kfr[kg] = row_frag(Kw, 16 * kg, kk, lane);
-          vfr[kg] = row_frag(Vw, 16 * kg, kk, lane);
-        }
+      auto sdp = [&](int kg) {
 #pragma unroll
         for (int fl = 0; fl < 2; ++fl) {
-          const bf16x8 qa = row_frag(Qs, 16 * fl, kk, lane);
-          const bf16x8 da = row_frag(Ds, 16 * fl, kk, lane);
-#pragma unroll
-          for (int kg = 0; kg < 2; ++kg) {
-            s[kg][fl] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kfr[kg], s[kg][fl], 0, 0, 0);
-            dp[kg][fl] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, vfr[kg], dp[kg][fl], 0, 0, 0);
-          }
+          s[kg][fl] = f32x4{0.f, 0.f, 0.f, 0.f};
+          dp[kg][fl] = nd4[fl];
         }
-      }
-      auto elementwise = [&](auto diag_c) {
-        constexpr bool DIAG = decltype(diag_c)::value;
 #pragma unroll
-        for (int kg = 0; kg < 2; ++kg) {
-          const int key = k_lo + 16 * kg + (lane & 15);
-          // the scores' affine part in place, as packed FMA pairs (v_pk_fma_f32; no register beyond s): x = s * sl2 - lse
+        for (int kk = 0; kk < 2; ++kk) {
+          const bf16x8 kf = row_frag(Kw, 16 * kg, kk, lane), vf = row_frag(Vw, 16 * kg, kk, lane);
 #pragma unroll
-          for (int fl = 0; fl < 2; ++fl)
-#pragma unroll
-            for (int r = 0; r < 4; r += 2) {
-              const f32x2 t = __builtin_elementwise_fma(f32x2{s[kg][fl][r], s[kg][fl][r + 1]}, f32x2{sl2, sl2},
-                                                        f32x2{nl4[fl][r], nl4[fl][r + 1]});
-              s[kg][fl][r] = t[0];
-              s[kg][fl][r + 1] = t[1];
-            }
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            uint32_t km[2] = {~0u, ~0u};
-            if constexpr (DROP) {
-              uint32_t pv = pre_t;
-              asm volatile("" : "+v"(pv));  // hashed here, not hoisted ahead of the tile (its masks would not fit)
-              drop_keep_masks(tk2, drop_fin(pv + ((uint32_t)r * (uint32_t)T + 16u * kg) * kDropC1, seed_kx(seed)),
-                              km[0], km[1]);
-            }
-#pragma unroll
-            for (int fl = 0; fl < 2; ++fl) {
-              float p = __builtin_amdgcn_exp2f(s[kg][fl][r]);
-              if constexpr (DIAG) p = (q0 + 16 * fl + 4 * g + r < key) ? 0.f : p;
-              float pdv = p, d = dp[kg][fl][r];
-              if constexpr (DROP) {
-                pdv = __uint_as_float(km[fl] & __float_as_uint(p));
-                d = sel_mask(km[fl], d, nd4[fl][r]);
-              }
-              dp[kg][fl][r] = pdv;
-              s[kg][fl][r] = p * d;
-            }
+          for (int fl = 0; fl < 2; ++fl) {
+            const bf16x8 qa = row_frag(Qs, 16 * fl, kk, lane);
+            const bf16x8 da = row_frag(Ds, 16 * fl, kk, lane);
+            s[kg][fl] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf, s[kg][fl], 0, 0, 0);
+            dp[kg][fl] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, vf, dp[kg][fl], 0, 0, 0);
           }
         }
       };
-      if (diag) elementwise(std::true_type{});
-      else elementwise(std::false_type{});
-      const bf16x8 p0 = pack_perm(dp[0], 0), p1 = pack_perm(dp[1], 0);
-      const bf16x8 s0 = pack_perm(s[0], 0), s1 = pack_perm(s[1], 0);
+      auto elem = [&](int kg) {
+        const int key = k_lo + 16 * kg + (lane & 15);
 #pragma unroll
-      for (int fd = 0; fd < 4; ++fd) {
-        const bf16x8 dot = tr_frag(Ds, 0, 16 * fd, lane);
-        const bf16x8 qt = tr_frag(Qs, 0, 16 * fd, lane);
-        dv[0][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dot, p0, dv[0][fd], 0, 0, 0);
-        dv[1][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dot, p1, dv[1][fd], 0, 0, 0);
-        dk[0][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qt, s0, dk[0][fd], 0, 0, 0);
-        dk[1][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qt, s1, dk[1][fd], 0, 0, 0);
+        for (int fl = 0; fl < 2; ++fl)
+#pragma unroll
+          for (int r = 0; r < 4; r += 2) {
+            const f32x2 t = __builtin_elementwise_fma(f32x2{s[kg][fl][r], s[kg][fl][r + 1]}, f32x2{sl2, sl2},
+                                                      f32x2{nl4[fl][r], nl4[fl][r + 1]});
+            s[kg][fl][r] = t[0];
+            s[kg][fl][r + 1] = t[1];
+          }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          uint32_t km[2] = {~0u, ~0u};
+          if constexpr (DROP) {
+            uint32_t pv = pre_t;
+            asm volatile("" : "+v"(pv));  // hashed here, not hoisted ahead of the tile (its masks would not fit)
+            drop_keep_masks(tk2, drop_fin(pv + ((uint32_t)r * (uint32_t)T + 16u * kg) * kDropC1, seed_kx(seed)),
+                            km[0], km[1]);
+          }
+#pragma unroll
+          for (int fl = 0; fl < 2; ++fl) {
+            float p = __builtin_amdgcn_exp2f(s[kg][fl][r]);
+            if constexpr (DIAG) p = (q0 + 16 * fl + 4 * g + r < key) ? 0.f : p;
+            float pdv = p, d = dp[kg][fl][r];
+            if constexpr (DROP) {
+              pdv = __uint_as_float(km[fl] & __float_as_uint(p));
+              d = sel_mask(km[fl], d, nd4[fl][r]);
+            }
+            dp[kg][fl][r] = pdv;
+            s[kg][fl][r] = p * d;
+          }
+        }
+      };
+      auto dvdk = [&](int kg) {
+        const bf16x8 pp = pack_perm(dp[kg], 0), ss = pack_perm(s[kg], 0);
+#pragma unroll
+        for (int fd = 0; fd < 4; ++fd) {
+          const bf16x8 dot = tr_frag(Ds, 0, 16 * fd, lane);
+          const bf16x8 qt = tr_frag(Qs, 0, 16 * fd, lane);
+          dv[kg][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dot, pp, dv[kg][fd], 0, 0, 0);
+          dk[kg][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qt, ss, dk[kg][fd], 0, 0, 0);
+        }
+      };
+#if ATTN_DKDV_PIPE == 1  // program order by phase, the scheduler free within the block
+      sdp(0);
+      sdp(1);
+      elem(0);
+      elem(1);
+      dvdk(0);
+      dvdk(1);
+#elif ATTN_DKDV_PIPE == 2  // program order by key group
+      sdp(0);
+      sdp(1);
+      elem(0);
+      dvdk(0);
+      elem(1);
+      dvdk(1);
+#elif ATTN_DKDV_PIPE == 4  // phases fenced (register-pressure check)
+      sdp(0);
+      __builtin_amdgcn_sched_barrier(0);
+      sdp(1);
+      __builtin_amdgcn_sched_barrier(0);
+      elem(0);
+      __builtin_amdgcn_sched_barrier(0);
+      dvdk(0);
+      __builtin_amdgcn_sched_barrier(0);
+      elem(1);
+      __builtin_amdgcn_sched_barrier(0);
+      dvdk(1);
+#else  // 3: key-group pipeline with the MFMAs of one group spread through the other group's elementwise
+      sdp(0);
+      __builtin_amdgcn_sched_barrier(0);
+      sdp(1);
+      elem(0);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, ATTN_DKDV_FILL, 0);  // VALU
       }
-    }
-    if (i + 1 < nqt) sstore(stg + (cur ^ 1) * kStage);
-    __syncthreads();
-  }
+      __builtin_amdgcn_sched_barrier(0);
+      dvdk(0);
+      elem(1);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+        __builtin_amdgcn_sched_group_barrier(0x002, ATTN_DKDV_FILL, 1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      dvdk(1);
+#endif
+    };
+    tile();
+  };
+  for (int i = i0 + 4; i < nqt; ++i) step(i, steady);
+#endif
   if (!wave_valid) return;
 #pragma unroll
   for (int kg = 0; kg < 2; ++kg) {

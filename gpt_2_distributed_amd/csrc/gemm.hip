@@ -349,6 +349,56 @@ GPT2MI_EXPORT int gpt2mi_gemm_wgrad(int M, int N, int K, const uint16_t* A, int 
   return gpt2mi::splitk_reduce(workspace, splits, (size_t)M * N, C, accumulate, s);
 }
 
+// Up to four weight gradients over the same K tokens as ONE split-K launch plus one reduction launch (a GPT2Block's qkv /
+// proj / fc1 / fc2 weight gradients, issued together at the end of the block's backward): C_g[M_g][N_g] (+)= alpha *
+// A_g^T B_g for g < count, every M_g and N_g a multiple of 256. Each problem's `splits` slabs are summed in split
+// order, so each C_g holds the same bits as gpt2mi_gemm_wgrad(M_g, N_g, K, ..., splits) with fp32 slabs.
+GPT2MI_EXPORT int gpt2mi_gemm_wgrad_grouped(int count, const int* M, const int* N, int K, const uint16_t* const* A,
+                                            const int* lda, const uint16_t* const* B, const int* ldb, float* const* C,
+                                            int accumulate, float alpha, const float* alpha_dev, float* workspace,
+                                            size_t workspace_floats, int splits, int sched, void* stream) {
+  GPT2MI_REQUIRE(count >= 1 && count <= kGroupMax, "gemm_wgrad_grouped: count=%d (1..%d)", count, kGroupMax);
+  GPT2MI_REQUIRE(K % 128 == 0 && K > 0, "gemm_wgrad_grouped: K=%d must be a multiple of 128", K);
+  GPT2MI_REQUIRE(splits >= 1 && splits <= K / 128, "gemm_wgrad_grouped: bad splits %d", splits);
+  GPT2MI_REQUIRE((sched & ~(GPT2MI_SCHED_NO_PERSISTENT | GPT2MI_SCHED_SHARED_CUS)) == 0,
+                 "gemm_wgrad_grouped: bad sched %#x (fp32 slabs on the ping-pong kernel only)", sched);
+  GemmGroup G{};
+  G.count = count;
+  const int ktiles = K / 64;
+  int tiles_per = (ktiles + splits - 1) / splits;
+  tiles_per += tiles_per & 1;  // even K-tile counts per split (the ping-pong kernel walks K-tile pairs)
+  const int kps = tiles_per * 64;
+  splits = (K + kps - 1) / kps;
+  size_t off = 0;
+  const float* slab[kGroupMax];
+  float* out[kGroupMax];
+  size_t n[kGroupMax];
+  for (int g = 0; g < count; ++g) {
+    GPT2MI_REQUIRE(M[g] > 0 && N[g] > 0 && M[g] % 256 == 0 && N[g] % 256 == 0,
+                   "gemm_wgrad_grouped: problem %d is %d x %d (multiples of 256 only)", g, M[g], N[g]);
+    GemmParams& P = G.p[g];
+    P.A = (const bf16*)A[g];
+    P.B = (const bf16*)B[g];
+    P.M = M[g]; P.N = N[g]; P.K = K; P.lda = lda[g]; P.ldb = ldb[g]; P.ldc = N[g];
+    P.alpha = alpha;
+    P.alpha_dev = alpha_dev;
+    P.k_per_split = kps;
+    P.C = workspace + off;
+    slab[g] = workspace + off;
+    out[g] = C[g];
+    n[g] = (size_t)M[g] * N[g];
+    off += (size_t)splits * n[g];
+    G.prefix[g + 1] = G.prefix[g] + (M[g] / 256) * (N[g] / 256);
+  }
+  G.tiles = G.prefix[count];
+  GPT2MI_REQUIRE(workspace != nullptr && workspace_floats >= off,
+                 "gemm_wgrad_grouped: workspace of %zu floats < %zu (splits x the problems' outputs)", workspace_floats, off);
+  hipStream_t s = (hipStream_t)stream;
+  int rc = gpt2mi::gemm_pp_grouped(G, s);
+  if (rc) return rc;
+  return gpt2mi::splitk_reduce_grouped(slab, out, n, count, splits, accumulate, s);
+}
+
 // The same weight gradient with the second operand given TRANSPOSED, k-contiguous: Bt stored [N][K] (X^T, e.g. the
 // final LayerNorm's output transposed once per step). Runs the ping-pong kernel in layout 1 on C^T[N][M] = Bt . A
 // (k-contiguous A operand, m-contiguous B operand: one transposed fragment stream instead of two; the lm_head wgrad

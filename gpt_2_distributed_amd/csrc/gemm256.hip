@@ -277,6 +277,34 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
 }
 
+// The same sums for the problems of a grouped weight-gradient launch (gpt2mi_gemm_wgrad_grouped): blockIdx.y is the
+// problem, whose slabs / output / length come from the kernel arguments; the same per-element order as above
+struct ReduceGroup {
+  const float* slab[kGroupMax];
+  float* out[kGroupMax];
+  size_t n4[kGroupMax];
+};
+__global__ __launch_bounds__(256) void splitk_reduce_grouped_kernel(ReduceGroup R, int splits, int accumulate) {
+  const int g = blockIdx.y;
+  const f32x4* s4 = reinterpret_cast<const f32x4*>(R.slab[g]);
+  f32x4* o4 = reinterpret_cast<f32x4*>(R.out[g]);
+  const size_t n4 = R.n4[g];
+  for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
+    f32x4 s = accumulate ? o4[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int z = 0; z < splits; z += 8) {
+      const int nz = min(8, splits - z);  // (uniform)
+      f32x4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (u < nz) v[u] = s4[(size_t)(z + u) * n4 + i];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (u < nz) s += v[u];
+    }
+    o4[i] = s;
+  }
+}
+
 // bf16 slabs (GPT2MI_SCHED_BF16_SLABS): 8 elements per thread (one 16-B load per slab), each widened to fp32 and added
 // in the order above (the old value first when accumulating, then the slabs in split order)
 __global__ __launch_bounds__(256) void splitk_reduce16_kernel(const bf16* __restrict__ slab, int splits, size_t n8,
@@ -378,6 +406,17 @@ int splitk_reduce16_t(const bf16* slab, int splits, int rows, int cols, float* o
 int splitk_reduce16(const bf16* slab, int splits, size_t n, float* out, int accumulate, hipStream_t s) {
   splitk_reduce16_kernel<<<2048, 256, 0, s>>>(slab, splits, n / 8, out, accumulate);
   return check_launch("splitk_reduce16");
+}
+int splitk_reduce_grouped(const float* const* slab, float* const* out, const size_t* n, int count, int splits,
+                          int accumulate, hipStream_t s) {
+  ReduceGroup R{};
+  for (int g = 0; g < count; ++g) {
+    R.slab[g] = slab[g];
+    R.out[g] = out[g];
+    R.n4[g] = n[g] / 4;
+  }
+  splitk_reduce_grouped_kernel<<<dim3(2048 / count, count), 256, 0, s>>>(R, splits, accumulate);
+  return check_launch("splitk_reduce_grouped");
 }
 int splitk_reduce(const float* slab, int splits, size_t n, float* out, int accumulate, hipStream_t s) {
   splitk_reduce_kernel<<<2048, 256, 0, s>>>(slab, splits, n / 4, out, accumulate);

@@ -72,6 +72,32 @@ __device__ __forceinline__ void gelu4(f32x4 u, f32x4 m, f32x4& h, f32x4& d) {
   }
 }
 
+// GELU_MOVE_EXP (A/B timing builds only): 1 = the fc1 epilogue stores u (bf16) in aux instead of
+// keep/(1-p) * gelu'(u), and the fc2 dgrad epilogue forms keep/(1-p) * gelu'(u) from it (sigmoid, derivative, the
+// site's dropout hash at p = 0.1) before its multiply: the derivative's VALU moved from the fc1 epilogue to the fc2 dgrad's
+#ifndef GELU_MOVE_EXP
+#define GELU_MOVE_EXP 0
+#endif
+GPT2MI_PRODUCT_KNOB(GELU_MOVE_EXP, 0);
+// h only (GELU_MOVE_EXP): h = u s m
+__device__ __forceinline__ f32x4 gelu4h(f32x4 u, f32x4 m) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f, m2log2e = -2.0f * 1.4426950408889634f;
+  const f32x2 A = {k0 * m2log2e, k0 * m2log2e}, B = {k0 * k1 * m2log2e, k0 * k1 * m2log2e}, one = {1.f, 1.f};
+  f32x4 h;
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const f32x2 x = {u[2 * p], u[2 * p + 1]}, mm = {m[2 * p], m[2 * p + 1]};
+    const f32x2 arg = x * __builtin_elementwise_fma(x * x, B, A);
+    const f32x2 e = {__builtin_amdgcn_exp2f(arg[0]), __builtin_amdgcn_exp2f(arg[1])};
+    const f32x2 den = e + one;
+    const f32x2 sg = {__builtin_amdgcn_rcpf(den[0]), __builtin_amdgcn_rcpf(den[1])};
+    const f32x2 hh = x * (sg * mm);
+    h[2 * p] = hh[0];
+    h[2 * p + 1] = hh[1];
+  }
+  return h;
+}
+
 // 4-element vector load/store of the activation element type TE (bf16 under autocast, fp32 in the
 // fp32 / no-autocast mode of the reference).
 // Epilogue stores are non-temporal (global_store ... nt): the outputs stream to HBM without displacing the
@@ -217,12 +243,29 @@ __device__ __forceinline__ void epilogue8(const GemmParams& P, int gm, int gn, f
       m0 = drop_scale4(P, pidx);
       m1 = drop_scale4(P, pidx + 2);
     }
-    gelu4(v0, m0, h0, d0);
-    gelu4(v1, m1, h1, d1);
+    if constexpr (GELU_MOVE_EXP == 1) {
+      h0 = gelu4h(v0, m0);
+      h1 = gelu4h(v1, m1);
+      d0 = v0;
+      d1 = v1;
+    } else {
+      gelu4(v0, m0, h0, d0);
+      gelu4(v1, m1, h1, d1);
+    }
     store8_bf16(reinterpret_cast<bf16*>(P.aux) + out_idx(gm, P.ldaux, gn), d0, d1);
     store8_bf16(C, h0, h1);
     r0 = h0;
     r1 = h1;
+  } else if constexpr (GELU_MOVE_EXP == 1) {
+    const uint32_t pidx = (uint32_t)gm * (uint32_t)(P.N >> 1) + (uint32_t)(gn >> 1);
+    GemmParams Q = P;
+    Q.thr = 6554u;  // the fc1 site's p = 0.1 (timing build)
+    Q.inv_keep = 1.f / 0.9f;
+    const f32x4 m0 = drop_scale4(Q, pidx), m1 = drop_scale4(Q, pidx + 2);
+    f32x4 h0, d0, h1, d1;
+    gelu4(f32x4{bf2f(op[0]), bf2f(op[1]), bf2f(op[2]), bf2f(op[3])}, m0, h0, d0);
+    gelu4(f32x4{bf2f(op[4]), bf2f(op[5]), bf2f(op[6]), bf2f(op[7])}, m1, h1, d1);
+    widen8(store8_bf16(C, v0 * d0, v1 * d1), r0, r1);
   } else {
     // vector products: packed (v_pk_mul_f32) whether or not the compiler's SLP pass runs
     const f32x4 o0 = v0 * f32x4{bf2f(op[0]), bf2f(op[1]), bf2f(op[2]), bf2f(op[3])};
@@ -236,7 +279,20 @@ __device__ __forceinline__ void epilogue_store(const GemmParams& P, int gm, int 
   epilogue_apply<EPI, TE>(P, gm, gn, v, epilogue_operand<EPI, TE>(P, gm, gn));
 }
 
+// Grouped weight gradients: kGroupMax problems at most, one launch (gemm_pp.hip gemm_pp_grouped_kernel); prefix[g] =
+// output tiles of problems 0 .. g-1 (prefix[count] = tiles)
+constexpr int kGroupMax = 4;
+struct GemmGroup {
+  GemmParams p[kGroupMax];
+  int prefix[kGroupMax + 1];
+  int count, tiles;
+};
+
 namespace gpt2mi {
+int gemm_pp_grouped(const GemmGroup& G, hipStream_t s);
+// out_g[i] (+)= sum_z slab_g[z][i] for every problem g of a grouped launch (fp32 slabs)
+int splitk_reduce_grouped(const float* const* slab, float* const* out, const size_t* n, int count, int splits,
+                          int accumulate, hipStream_t s);
 int gemm256_dispatch(int layout, int epilogue, const GemmParams& P, hipStream_t s, int splits);
 // persistent_ok: the caller allows the persistent (one block per CU) schedule (gpt2mi.h GPT2MI_SCHED_NO_PERSISTENT);
 // shared_cus: other kernels (RCCL) may hold CUs: the persistent shapes take their tiles from work queues

@@ -32,6 +32,7 @@ HBM layout per (B, T) workspace (M = B*T tokens, C = n_embd, Vp = vocab padded t
 """
 from __future__ import annotations
 
+import os
 import weakref
 from dataclasses import dataclass
 from typing import Dict, List, Optional
@@ -40,6 +41,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _lib as K
+from ._lib import wgrad_group_splits as K_wgrad_group_splits
 from ._lib import wgrad_splits as K_wgrad_splits
 from .dropout_keys import MULTIPLIERS
 
@@ -151,6 +153,9 @@ class Scratch:
         wshapes = [(3 * C, C), (C, C), (4 * C, C), (C, 4 * C)] + ([(vpad, C)] if head else [])
         need = max((K_wgrad_splits(m, n, M) * m * n if K_wgrad_splits(m, n, M) > 1 else 0)
                    for m, n in wshapes) if C % 64 == 0 and act == BF16 else 0
+        if C % 256 == 0 and act == BF16 and M % 128 == 0:  # a block's grouped weight gradients (Engine._wgrad_group)
+            for gsh in (wshapes[2:4], wshapes[:2]):  # fc1 + fc2, qkv + proj
+                need = max(need, K_wgrad_group_splits(gsh, M) * sum(m * n for m, n in gsh))
         if head and C % 64 == 0 and act == BF16 and M % 128 == 0 and vpad % 256 == 0:
             # the lm_head's transposed-X wgrad (taken under exactly these conditions, Engine._backward) always goes
             # through its slabs
@@ -746,28 +751,56 @@ class Engine:
         else:
             self._gemm(K.DGRAD, epi, M, n_in, n_out, dy, n_out, self.w(wname, act), n_in, out, n_in, **kw)
 
-    def _mlp_bwd(self, l, A, S, dY, dx_out, M, act):
+    # A GPT2Block's four weight gradients as two grouped launches (gpt2mi_gemm_wgrad_grouped: one split-K launch + one
+    # reduction each), each issued right after the dgrad that finishes its operands: fc2 + fc1 after the fc1 dgrad
+    # (72 tiles x 7 splits at GPT-2 124M: 1.97 rounds of 256 CUs), proj + qkv after the qkv dgrad (36 x 7: one round),
+    # instead of four launches at 9 / 28 / 7 / 7 splits with four reductions. Same operands, fewer slab bytes to reduce
+    # (proj at 7 splits instead of 28): block weight gradients + reductions 9.43 -> 9.27 ms a step (profiles/r6d/).
+    # One group of all four at the end of the block (round 6's first build, which needs a second buffer for the proj
+    # branch's gradient) measured the same (profiles/r6c/). bf16 autocast with fp32 slabs, widths multiples of 256.
+    # GPT2MI_GROUP_WGRADS=0: the four launches (same-box A/B runs of the step).
+    GROUP_WGRADS = os.environ.get("GPT2MI_GROUP_WGRADS", "1") != "0"
+
+    def _group_ok(self, act, M) -> bool:
+        return self.GROUP_WGRADS and act == BF16 and self.cfg.n_embd % 256 == 0 and M % 128 == 0 and \
+            not self.wgrad_bf16_slabs
+
+    def _wgrad_or_defer(self, S, act, m, n, M, a, lda, b, ldb, out, defer):
+        if defer is None:
+            self._wgrad(S, act, m, n, M, a, lda, b, ldb, out)
+        else:
+            defer.append((m, n, a, lda, b, ldb, out))
+
+    def _wgrad_group(self, S, M, probs):
+        with self._probe("wgrad"):
+            K.gemm_wgrad_grouped(probs, M, accumulate=not self._grad_fresh, workspace=S.wgrad_ws,
+                                 splits=K_wgrad_group_splits([(q[0], q[1]) for q in probs], M), sched=self._sched())
+
+    def _mlp_bwd(self, l, A, S, dY, dx_out, M, act, defer=None):
         """dY = grad of the fc2 output with drop2 applied (its bias grad already taken) -> dx_out = grad of
-        the MLP input (bf16), weight grads of fc1/fc2 and the fc1 bias grad."""
+        the MLP input (bf16), weight grads of fc1/fc2 (or their problems appended to ``defer``) and the fc1 bias grad."""
         C = self.cfg.n_embd
         pre = f"transformer.h.{l}."
         self._dgrad(act, M, S.dU, dY, pre + "mlp.fc2.weight", 4 * C, C, K.EPI_GELU_BWD, aux=A.dgelu, ldaux=4 * C,
                     dbias=self.g(pre + "mlp.fc1.bias"))
-        self._wgrad(S, act, C, 4 * C, M, dY, C, A.h, 4 * C, self.g(pre + "mlp.fc2.weight"))
+        self._wgrad_or_defer(S, act, C, 4 * C, M, dY, C, A.h, 4 * C, self.g(pre + "mlp.fc2.weight"), defer)
         self._dgrad(act, M, dx_out, S.dU, pre + "mlp.fc1.weight", C, 4 * C)
-        self._wgrad(S, act, 4 * C, C, M, S.dU, 4 * C, A.ln2, C, self.g(pre + "mlp.fc1.weight"))
+        self._wgrad_or_defer(S, act, 4 * C, C, M, S.dU, 4 * C, A.ln2, C, self.g(pre + "mlp.fc1.weight"), defer)
+        if defer:  # fc2 + fc1, while their operands are the latest written
+            self._wgrad_group(S, M, defer)
+            defer.clear()
 
-    def _attn_bwd(self, l, A, S, dY, dx_out, B, T, act, pa, seeds):
+    def _attn_bwd(self, l, A, S, dY, dx_out, B, T, act, pa, seeds, defer=None):
         """dY = grad of the proj output with resid_drop applied -> dx_out = grad of the attention input."""
         C, H = self.cfg.n_embd, self.cfg.n_head
         M = B * T
         pre = f"transformer.h.{l}."
         self._dgrad(act, M, dx_out, dY, pre + "attn.proj.weight", C, C)
-        self._wgrad(S, act, C, C, M, dY, C, A.ao, C, self.g(pre + "attn.proj.weight"))
+        self._wgrad_or_defer(S, act, C, C, M, dY, C, A.ao, C, self.g(pre + "attn.proj.weight"), defer)
         K.attn_bwd(A.qkv, A.ao, dx_out, A.lse, S.delta, S.dqkv, B, T, H, C // H, pa, seeds[("attn", l)],
                    colsum=S.dqkv_cs)
         self._dgrad(act, M, dx_out, S.dqkv, pre + "attn.qkv.weight", C, 3 * C)
-        self._wgrad(S, act, 3 * C, C, M, S.dqkv, 3 * C, A.ln1, C, self.g(pre + "attn.qkv.weight"))
+        self._wgrad_or_defer(S, act, 3 * C, C, M, S.dqkv, 3 * C, A.ln1, C, self.g(pre + "attn.qkv.weight"), defer)
         if S.dqkv_cs is not None:  # qkv bias grad: sum the attention backward's 32-token partials
             K.colsum_bf16(S.dqkv_cs, self.g(pre + "attn.qkv.bias"), M // 32, 3 * C, 3 * C)
         else:
@@ -779,11 +812,14 @@ class Engine:
         C = self.cfg.n_embd
         M = B * T
         pre = f"transformer.h.{l}."
-        self._mlp_bwd(l, A, S, S.dres_bf, S.dln, M, act)
+        grp = [] if self._group_ok(act, M) else None
+        self._mlp_bwd(l, A, S, S.dres_bf, S.dln, M, act, grp)
         K.layernorm_bwd(A.xmid, self.p(pre + "ln2.weight"), A.m2, A.r2, S.dln, S.dres, self.g(pre + "ln2.weight"),
                         self.g(pre + "ln2.bias"), S.dres_bf, self.g(pre + "attn.proj.bias"), M, C, pr,
                         seeds[("proj", l)])
-        self._attn_bwd(l, A, S, S.dres_bf, S.dln, B, T, act, pa, seeds)
+        self._attn_bwd(l, A, S, S.dres_bf, S.dln, B, T, act, pa, seeds, grp)
+        if grp:  # proj + qkv, before LN1's backward overwrites dres_bf (the proj weight gradient's operand)
+            self._wgrad_group(S, M, grp)
         if not last:
             K.layernorm_bwd(x_in, self.p(pre + "ln1.weight"), A.m1, A.r1, S.dln, S.dres,
                             self.g(pre + "ln1.weight"), self.g(pre + "ln1.bias"), S.dres_bf,

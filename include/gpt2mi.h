@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GPT2MI_ABI_VERSION 12
+#define GPT2MI_ABI_VERSION 13
 
 const char* gpt2mi_last_error(void);
 int gpt2mi_abi_version(void); /* returns GPT2MI_ABI_VERSION of the built library */
@@ -111,6 +111,16 @@ int gpt2mi_gemm_wgrad(int M, int N, int K, const uint16_t* A, int lda, const uin
 int gpt2mi_gemm_wgrad_kt(int M, int N, int K, const uint16_t* A, int lda, const uint16_t* Bt, int ldbt, float* C,
                          int ldc, int accumulate, float alpha, const float* alpha_dev, float* workspace,
                          size_t workspace_floats, int splits, int sched, void* stream);
+
+/* Grouped weight gradients (v13; train_gpt2_distributed.py:412, the autograd wgrads of a GPT2Block's four nn.Linear,
+ * model.py:131,135,172,175): for g < count (<= 4), C[g][M[g]][N[g]] (+)= alpha*(alpha_dev?) * A[g]^T B[g] over the same
+ * K tokens, as ONE split-K launch and ONE reduction launch. Host arrays of count entries; every M[g], N[g] a multiple of
+ * 256, K of 128, ldc == N[g]; workspace >= splits * sum(M[g]*N[g]) floats. Each C[g] gets the bits gpt2mi_gemm_wgrad
+ * gives it with the same `splits` and fp32 slabs. sched: GPT2MI_SCHED_AUTO or the CU-sharing flags (no BF16_SLABS). */
+int gpt2mi_gemm_wgrad_grouped(int count, const int* M, const int* N, int K, const uint16_t* const* A, const int* lda,
+                              const uint16_t* const* B, const int* ldb, float* const* C, int accumulate, float alpha,
+                              const float* alpha_dev, float* workspace, size_t workspace_floats, int splits, int sched,
+                              void* stream);
 
 /* K4-K8: causal flash attention, head_dim 64 — model.py:124-155. q/k/v read from qkv [B*T, 3C];
  * out [B*T, C] head-merged; lse [B*H, T] (natural log of the 1/sqrt(D)-scaled scores). */

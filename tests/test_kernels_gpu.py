@@ -783,6 +783,49 @@ def test_gemm_wgrad_kt_same_bits_as_wgrad(m, n, tokens, splits):
         assert rel_err(C2[rows].double().cpu(), ref.cpu()) < 1e-5
 
 
+@pytest.mark.parametrize("C,tokens", [(768, 65536), (768, 4096), (1024, 2048), (256, 1024)])
+def test_gemm_wgrad_grouped_same_bits_as_wgrad(C, tokens):
+    """gpt2mi_gemm_wgrad_grouped (ABI v13: a GPT2Block's qkv / proj / fc1 / fc2 weight gradients as one launch + one
+    reduction) against gpt2mi_gemm_wgrad of each problem with the same split-K factor (fp32 slabs): the same bits,
+    writing (lazy-zeroed arena) and accumulating, with alpha and a device alpha; sampled rows against float64; at C =
+    768 and 65 536 tokens the engine's shapes and split choice."""
+    shapes = [(3 * C, C), (C, C), (4 * C, C), (C, 4 * C)]
+    sp = L().wgrad_group_splits(shapes, tokens)
+    g = torch.Generator(device=dev).manual_seed(C + tokens)
+    ops = [((torch.randn(tokens, m, device=dev, generator=g) * 0.05).to(torch.bfloat16),
+            torch.randn(tokens, n, device=dev, generator=g).to(torch.bfloat16)) for m, n in shapes]
+    ws = torch.empty(sp * sum(m * n for m, n in shapes), device=dev)
+    ad = torch.tensor([0.75], device=dev)
+    C0 = [torch.randn(m, n, device=dev, generator=g) for m, n in shapes]
+    for acc in (False, True):
+        Cg = [c.clone() for c in C0]
+        probs = [(m, n, A, m, B, n, Cg[i]) for i, ((m, n), (A, B)) in enumerate(zip(shapes, ops))]
+        L().gemm_wgrad_grouped(probs, tokens, accumulate=acc, alpha=0.5, alpha_dev=ad, workspace=ws, splits=sp)
+        for i, ((m, n), (A, B)) in enumerate(zip(shapes, ops)):
+            Ci = C0[i].clone()
+            L().gemm_wgrad(m, n, tokens, A, m, B, n, Ci, n, accumulate=acc, alpha=0.5, alpha_dev=ad, workspace=ws,
+                           splits=sp)
+            torch.cuda.synchronize()
+            assert torch.equal(Ci, Cg[i]), (acc, i, (Ci - Cg[i]).abs().max().item())
+            rows = torch.cat([torch.arange(0, m, max(1, m // 12), device=dev), torch.arange(m - 4, m, device=dev)])
+            ref = 0.375 * (A[:, rows].double().t() @ B.double()) + (C0[i][rows].double() if acc else 0)
+            assert rel_err(Cg[i][rows].double().cpu(), ref.cpu()) < 1e-5
+    # fewer problems, and the argument checks
+    Cg = [c.clone() for c in C0[:2]]
+    L().gemm_wgrad_grouped([(m, n, A, m, B, n, Cg[i]) for i, ((m, n), (A, B)) in enumerate(zip(shapes[:2], ops))],
+                           tokens, accumulate=False, workspace=ws, splits=sp)
+    C1 = torch.empty_like(Cg[1])
+    L().gemm_wgrad(shapes[1][0], shapes[1][1], tokens, ops[1][0], shapes[1][0], ops[1][1], shapes[1][1], C1,
+                   shapes[1][1], accumulate=False, workspace=ws, splits=sp)
+    torch.cuda.synchronize()
+    assert torch.equal(C1, Cg[1])
+    with pytest.raises(L().KernelError, match="multiples of 256"):
+        L().gemm_wgrad_grouped([(192, 256, ops[0][0], 3 * C, ops[0][1], C, Cg[0])], tokens, workspace=ws, splits=sp)
+    with pytest.raises(L().KernelError, match="workspace"):
+        L().gemm_wgrad_grouped([(m, n, A, m, B, n, c) for (m, n), (A, B), c in zip(shapes, ops, C0)], tokens,
+                               workspace=ws[:16], splits=sp)
+
+
 @pytest.mark.parametrize("m,n", [(50432, 768), (2304, 768), (768, 3072)])
 def test_wgrad_full_size_vs_fp64(m, n):
     """The step's weight gradients at BASELINE cfg 2's full size (65 536 tokens, the split-K factor the engine picks)
