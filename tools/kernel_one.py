@@ -81,21 +81,29 @@ def make(name):
         dqkv = torch.empty(M, 3 * C, dtype=torch.bfloat16, device=dev)
         p = float(os.environ.get("ATTN_P", "0.1"))
         return lambda: K.attn_bwd(qkv, out, dout, lse, delta, dqkv, B, T, H, C // H, p, 5)
-    if name == "wgrad":  # one step's weight gradients: 12 x (qkv, proj, fc1, fc2) + the tied lm_head
-        shapes = 12 * [(3 * C, C), (C, C), (4 * C, C), (C, 4 * C)] + [(Vp, C)]
+    if name == "wgrad":  # one step's weight gradients: 12 x (fc2 + fc1, proj + qkv grouped) + the tied lm_head
+        pairs = [[(C, 4 * C), (4 * C, C)], [(C, C), (3 * C, C)]]  # as Engine._block_bwd groups them (round 6)
+        shapes = [sh for pr in pairs for sh in pr] + [(Vp, C)]
         ops = {(m, n): (r(M, m), r(M, n), torch.zeros(m, n, device=dev)) for m, n in set(shapes)}
-        ws = torch.empty(max(K.wgrad_splits(m, n, M) * m * n for m, n in shapes), device=dev)
-
+        ws = torch.empty(max([K.wgrad_splits(Vp, C, M) * Vp * C] +
+                             [K.wgrad_group_splits(pr, M) * sum(m * n for m, n in pr) for pr in pairs]), device=dev)
         xt = torch.empty(C, M, dtype=torch.bfloat16, device=dev)
+        grouped = not SLABS  # the opt-in bf16 slabs keep the four launches
 
         def run():  # the lm_head as the step runs it: lnf transposed, gpt2mi_gemm_wgrad_kt
-            for m, n in shapes:
-                a, x, g = ops[(m, n)]
-                if m == Vp:
-                    K.transpose_bf16(x, xt, M, C, C, M)
-                    K.gemm_wgrad_kt(m, n, M, a, m, xt, M, g, n, workspace=ws, splits=K.wgrad_splits(m, n, M), sched=SLABS)
-                else:
-                    K.gemm_wgrad(m, n, M, a, m, x, n, g, n, workspace=ws, splits=K.wgrad_splits(m, n, M), sched=SLABS)
+            a, x, g = ops[(Vp, C)]
+            K.transpose_bf16(x, xt, M, C, C, M)
+            K.gemm_wgrad_kt(Vp, C, M, a, Vp, xt, M, g, C, workspace=ws, splits=K.wgrad_splits(Vp, C, M), sched=SLABS)
+            for _ in range(12):
+                for pr in pairs:
+                    if grouped:
+                        K.gemm_wgrad_grouped([(m, n, ops[(m, n)][0], m, ops[(m, n)][1], n, ops[(m, n)][2])
+                                              for m, n in pr], M, workspace=ws, splits=K.wgrad_group_splits(pr, M))
+                    else:
+                        for m, n in pr:
+                            a, x, g = ops[(m, n)]
+                            K.gemm_wgrad(m, n, M, a, m, x, n, g, n, workspace=ws, splits=K.wgrad_splits(m, n, M),
+                                         sched=SLABS)
         return run
     raise SystemExit(f"unknown kernel {name}")
 

@@ -19,16 +19,16 @@ ALGO = {  # algorithmic bytes per launch (operands read once, outputs written on
     "lm_head_wgrad": 2 * (65536 * 50432 + 65536 * 768) + 4 * 2 * 50432 * 768,
     "fc1_fwd": 2 * (65536 * 768 + 3072 * 768 + 2 * 65536 * 3072) + 4 * 3072,
     "attn_fwd": 2 * (65536 * 2304 + 65536 * 768) + 4 * 768 * 1024,
-    # the weight-gradient family, averaged over one step's 49 launches: dY and X read once (bf16), dW read and
-    # written once (fp32, accumulated)
+    # the weight-gradient family, averaged over one step's 25 launches (the tied lm_head + each block's two grouped
+    # pairs since round 6; 49 launches before): dY and X read once (bf16), dW read and written once (fp32, accumulated)
     "wgrad": (12 * sum(2 * 65536 * (m + n) + 8 * m * n for m, n in ((2304, 768), (768, 768), (3072, 768), (768, 3072)))
-              + 2 * 65536 * (50432 + 768) + 8 * 50432 * 768) // 49,
+              + 2 * 65536 * (50432 + 768) + 8 * 50432 * 768) // 25,
 }
 # kernels whose counters make up one probed launch (the wgrad probe = split-K GEMM + slab reduction)
 KERNEL_KEY = {"attn_fwd": ("attn_fwd",), "lm_head_wgrad": ("gemm_pp", "splitk_reduce", "transpose_bf16"),
-              "wgrad": ("gemm_pp", "splitk_reduce")}  # (the lm_head's one lnf transpose per 49 launches: 0.4 %)
+              "wgrad": ("gemm_pp", "splitk_reduce")}  # (the lm_head's one lnf transpose per 25 launches: 0.7 %)
 # launches of one repetition of a family probe (the per-launch figure averages the last repetition's launches)
-FAMILY = {"wgrad": 49}
+FAMILY = {"wgrad": 25}
 
 
 def short(name):
