@@ -628,6 +628,103 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkdv_kernel(const bf16* __res
   __syncthreads();
   const char* Kw = Kl + 32 * w * 128;  // this wave's 32 keys
   const char* Vw = Vl + 32 * w * 128;
+#if ATTN_DKDV_PIPE == 0
+  for (int i = i0; i < nqt; ++i) {
+    const int cur = (i - i0) & 1;
+    const char* Qs = stg + cur * kStage;
+    const char* Ds = Qs + kTile;
+    const float* Ls = reinterpret_cast<const float*>(Qs + 2 * kTile);
+    const float* Dl = Ls + BQ3;
+    if (i + 1 < nqt) gload(i + 1, stg + (cur ^ 1) * kStage);
+    const int q0 = i * BQ3;
+    if (wave_valid && q0 + BQ3 - 1 >= k_lo) {
+      const bool diag = q0 < k_lo + 31;
+      const uint32_t pre_t = DROP ? drop_pre(seed32(seed), ((uint32_t)bh * T + q0 + 4 * g) * (uint32_t)T + k_lo + (lane & 15)) : 0u;
+      f32x4 s[2][2], dp[2][2];  // [kg][fl]: S[q = q0 + 16fl + 4g + r][key = k_lo + 16kg + (l&15)]
+      f32x4 nl4[2], nd4[2];  // -lse * log2(e), -delta of the tile's queries
+#pragma unroll
+      for (int fl = 0; fl < 2; ++fl) {
+        nl4[fl] = *reinterpret_cast<const f32x4*>(Ls + 16 * fl + 4 * g);
+        nd4[fl] = *reinterpret_cast<const f32x4*>(Dl + 16 * fl + 4 * g);
+        s[0][fl] = s[1][fl] = f32x4{0.f, 0.f, 0.f, 0.f};
+        dp[0][fl] = dp[1][fl] = nd4[fl];
+      }
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 kfr[2], vfr[2];
+#pragma unroll
+        for (int kg = 0; kg < 2; ++kg) {
+          kfr[kg] = row_frag(Kw, 16 * kg, kk, lane);
+          vfr[kg] = row_frag(Vw, 16 * kg, kk, lane);
+        }
+#pragma unroll
+        for (int fl = 0; fl < 2; ++fl) {
+          const bf16x8 qa = row_frag(Qs, 16 * fl, kk, lane);
+          const bf16x8 da = row_frag(Ds, 16 * fl, kk, lane);
+#pragma unroll
+          for (int kg = 0; kg < 2; ++kg) {
+            s[kg][fl] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kfr[kg], s[kg][fl], 0, 0, 0);
+            dp[kg][fl] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, vfr[kg], dp[kg][fl], 0, 0, 0);
+          }
+        }
+      }
+      auto elementwise = [&](auto diag_c) {
+        constexpr bool DIAG = decltype(diag_c)::value;
+#pragma unroll
+        for (int kg = 0; kg < 2; ++kg) {
+          const int key = k_lo + 16 * kg + (lane & 15);
+          // the scores' affine part in place, as packed FMA pairs (v_pk_fma_f32; no register beyond s): x = s * sl2 - lse
+#pragma unroll
+          for (int fl = 0; fl < 2; ++fl)
+#pragma unroll
+            for (int r = 0; r < 4; r += 2) {
+              const f32x2 t = __builtin_elementwise_fma(f32x2{s[kg][fl][r], s[kg][fl][r + 1]}, f32x2{sl2, sl2},
+                                                        f32x2{nl4[fl][r], nl4[fl][r + 1]});
+              s[kg][fl][r] = t[0];
+              s[kg][fl][r + 1] = t[1];
+            }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            uint32_t km[2] = {~0u, ~0u};
+            if constexpr (DROP) {
+              uint32_t pv = pre_t;
+              asm volatile("" : "+v"(pv));  // hashed here, not hoisted ahead of the tile (its masks would not fit)
+              drop_keep_masks(tk2, drop_fin(pv + ((uint32_t)r * (uint32_t)T + 16u * kg) * kDropC1, seed_kx(seed)),
+                              km[0], km[1]);
+            }
+#pragma unroll
+            for (int fl = 0; fl < 2; ++fl) {
+              float p = __builtin_amdgcn_exp2f(s[kg][fl][r]);
+              if constexpr (DIAG) p = (q0 + 16 * fl + 4 * g + r < key) ? 0.f : p;
+              float pdv = p, d = dp[kg][fl][r];
+              if constexpr (DROP) {
+                pdv = __uint_as_float(km[fl] & __float_as_uint(p));
+                d = sel_mask(km[fl], d, nd4[fl][r]);
+              }
+              dp[kg][fl][r] = pdv;
+              s[kg][fl][r] = p * d;
+            }
+          }
+        }
+      };
+      if (diag) elementwise(std::true_type{});
+      else elementwise(std::false_type{});
+      const bf16x8 p0 = pack_perm(dp[0], 0), p1 = pack_perm(dp[1], 0);
+      const bf16x8 s0 = pack_perm(s[0], 0), s1 = pack_perm(s[1], 0);
+#pragma unroll
+      for (int fd = 0; fd < 4; ++fd) {
+        const bf16x8 dot = tr_frag(Ds, 0, 16 * fd, lane);
+        const bf16x8 qt = tr_frag(Qs, 0, 16 * fd, lane);
+        dv[0][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dot, p0, dv[0][fd], 0, 0, 0);
+        dv[1][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dot, p1, dv[1][fd], 0, 0, 0);
+        dk[0][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qt, s0, dk[0][fd], 0, 0, 0);
+        dk[1][fd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qt, s1, dk[1][fd], 0, 0, 0);
+      }
+    }
+    if (i + 1 < nqt) sstore(stg + (cur ^ 1) * kStage);
+    __syncthreads();
+  }
+#else
   // one query tile: Q / dO / lse / delta of tile i are in stage (i - i0) & 1; the next tile is staged under it
   auto step = [&](int i, auto work) {
     const int cur = (i - i0) & 1;
@@ -727,9 +824,6 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkdv_kernel(const bf16* __res
         }
       }
   };
-#if ATTN_DKDV_PIPE == 0
-  for (int i = i0; i < nqt; ++i) step(i, general);
-#else
   // Tiles i0 .. i0 + 3 hold every wave's diagonal tile (wave w: i0 + w) and the inactive waves; from i0 + 4 on every
   // wave of the workgroup is active and off the diagonal, and the tile is ONE basic block: the S / dP MFMAs, the
   // elementwise chain and the dV / dK MFMAs scheduled together (key group kg = 0 finished first, its dS formed while

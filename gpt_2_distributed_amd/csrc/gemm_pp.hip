@@ -321,10 +321,39 @@ __device__ __forceinline__ void tile_of(int pid, int tiles_m, int tiles_n, int& 
 // per tile there). Layout-0 shapes without split-K only (host-selected).
 // BND: a transposed operand has a partial last tile (M or N not a multiple of 256): its DMA is bounded (dma_half)
 // DYN (PERSIST only): tiles from the work queue g_pp_queue (above) instead of the static walk
-// item0 >= 0: the block's (split, tile) item, given by a grouped launch (gemm_pp_grouped_kernel); -1: from blockIdx
-template <bool A_T, bool B_T, int EPI, int MAP, bool PERSIST = false, bool BND = false, bool DYN = false>
-__device__ __forceinline__ void gemm_pp_body(const GemmParams& P, const int item0) {
+// GRP: a grouped weight-gradient launch (gpt2mi_gemm_wgrad_grouped): up to kGroupMax problems with the same token count
+// and split, each a full-tile (M, N multiples of 256) weight gradient into its own slabs, as ONE launch over the (split,
+// problem tile) items, split-major like the single launch (the XCD remap gives each XCD a contiguous item range, so the
+// blocks of one split, which read the same token rows of the problems' operands, share an L2). A block finds its problem
+// from the tile prefix (wave-uniform, scalar loads of the kernel argument) and runs the single-problem code on it. The
+// kernel argument is the problem table then; P below is a reference into it (for GRP = false, to the one problem), so
+// the single-problem kernels compile exactly as before (a by-value copy or a device-function parameter made the
+// persistent residual kernels spill).
+template <bool GRP>
+using PPArg = typename std::conditional<GRP, GemmGroup, GemmParams>::type;
+template <bool GRP>
+__device__ __forceinline__ const GemmParams& pp_problem(const PPArg<GRP>& a, int& item) {
+  if constexpr (GRP) {
+    const int nsplit = (a.p[0].K + a.p[0].k_per_split - 1) / a.p[0].k_per_split;
+    const int it = xcd_remap(blockIdx.x, a.tiles * nsplit);
+    const int split = it / a.tiles, t = it - split * a.tiles;
+    int g = 0;
+#pragma unroll
+    for (int k = 1; k < kGroupMax; ++k)
+      if (k < a.count && t >= a.prefix[k]) g = k;
+    item = split * (a.prefix[g + 1] - a.prefix[g]) + (t - a.prefix[g]);
+    return a.p[g];
+  } else {
+    item = -1;
+    return a;
+  }
+}
+template <bool A_T, bool B_T, int EPI, int MAP, bool PERSIST = false, bool BND = false, bool DYN = false,
+          bool GRP = false>
+__global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(PPArg<GRP> KA) {
   PP_STAMP(0)
+  int item0;
+  const GemmParams& P = pp_problem<GRP>(KA, item0);
   constexpr bool AIL = MAP & 1, BIL = MAP & 2;  // interleaved half-tile maps (A/B experiments)
   static_assert(!PERSIST || MAP == 0, "the persistent epilogue assumes the contiguous half-tile map");
   // phase-4 B reads (see ktile): the persistent schedule and the weight gradients (both operands by buffer DMA); the
@@ -1012,27 +1041,6 @@ write_image(mi, wr * 64);
   }  // tile loop
 }
 
-template <bool A_T, bool B_T, int EPI, int MAP, bool PERSIST = false, bool BND = false, bool DYN = false>
-__global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams P) {
-  gemm_pp_body<A_T, B_T, EPI, MAP, PERSIST, BND, DYN>(P, -1);
-}
-
-// Grouped split-K weight gradients (gpt2mi_gemm_wgrad_grouped): up to kGroupMax problems with the same token count and
-// split, each a full-tile (M, N multiples of 256) weight gradient into its own slabs, as ONE launch over the (split,
-// problem tile) items, split-major like the single launch (the XCD remap gives each XCD a contiguous item range, so
-// the blocks of one split, which read the same token rows of the four operand pairs, share an L2). A block finds its
-// problem from the tile prefix (wave-uniform, scalar) and runs the single-problem body on that problem's parameters.
-__global__ __launch_bounds__(kThreads, 1) void gemm_pp_grouped_kernel(GemmGroup G) {
-  const int nsplit = (G.p[0].K + G.p[0].k_per_split - 1) / G.p[0].k_per_split;
-  const int it = xcd_remap(blockIdx.x, G.tiles * nsplit);
-  const int split = it / G.tiles, t = it - split * G.tiles;
-  int g = 0;
-#pragma unroll
-  for (int k = 1; k < kGroupMax; ++k)
-    if (k < G.count && t >= G.prefix[k]) g = k;
-  const int nt = G.prefix[g + 1] - G.prefix[g];
-  gemm_pp_body<true, true, EPI_SLAB, 3>(G.p[g], split * nt + (t - G.prefix[g]));
-}
 
 // Default half-tile maps: interleaved for m-contiguous (transposed) operands, contiguous otherwise
 // (measured, tools/gemm_probe.py: 8192^3 dgrad 1195 vs 1022 TF with B interleaved; no effect on the
@@ -1054,7 +1062,7 @@ int launch(const GemmParams& P, hipStream_t s, int splits) {
 namespace gpt2mi {
 int gemm_pp_grouped(const GemmGroup& G, hipStream_t s) {
   const int nsplit = (G.p[0].K + G.p[0].k_per_split - 1) / G.p[0].k_per_split;
-  gemm_pp_grouped_kernel<<<dim3(G.tiles * nsplit), kThreads, 0, s>>>(G);
+  gemm_pp_kernel<true, true, EPI_SLAB, 3, false, false, false, true><<<dim3(G.tiles * nsplit), kThreads, 0, s>>>(G);
   return gpt2mi::check_launch("gemm_pp_grouped");
 }
 }  // namespace gpt2mi
