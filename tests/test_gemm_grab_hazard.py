@@ -84,7 +84,9 @@ def _vmcnt0(s):
 @pytest.mark.skipif(not shutil.which(HIPCC) and not os.path.exists(HIPCC), reason="hipcc not available")
 def test_work_queue_grab_register_untouched_until_retired():
     funcs = _functions(_asm())
-    dyn = {n: b for n, b in funcs.items() if "gemm_pp_kernel" in n and n.endswith("ELb1EEEv10GemmParams")}
+    # template arguments <A_T, B_T, EPI, MAP, PERSIST, BND, DYN, GRP>: DYN = 1 (GRP = 0, the single-problem kernels)
+    dyn = {n: b for n, b in funcs.items()
+           if re.search(r"gemm_pp_kernelILb[01]ELb[01]ELi\d+ELi\d+ELb[01]ELb[01]ELb1ELb0E", n)}
     assert dyn, "no DYN (work-queue) kernel found"
     checked = 0
     for name, body in dyn.items():
