@@ -46,6 +46,9 @@ constexpr int BKB = 128;  // keys per workgroup in dK/dV (4 waves of 32)
 #define ATTN_DKDV_FILL 10  // ATTN_DKDV_PIPE 3: VALU instructions placed after each MFMA
 #endif
 GPT2MI_PRODUCT_KNOB(ATTN_DKDV_PIPE, 0);
+#ifndef ATTN_HASH_ANCHOR
+#define ATTN_HASH_ANCHOR 0  // dK/dV dropout hash: 1 = the opaque anchor on the counter sum (no v_mov per hash; A/B)
+#endif
 constexpr int kThreads = 256;
 constexpr float kLog2e = 1.4426950408889634f;
 
@@ -687,10 +690,19 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkdv_kernel(const bf16* __res
           for (int r = 0; r < 4; ++r) {
             uint32_t km[2] = {~0u, ~0u};
             if constexpr (DROP) {
+#if ATTN_HASH_ANCHOR
+              // the counter of this (r, kg) formed, then made opaque: hashed here, not hoisted ahead of the tile (its
+              // masks would not fit), and the add writes a fresh register (no copy of pre_t per hash)
+              const uint32_t off = __builtin_amdgcn_readfirstlane(((uint32_t)r * (uint32_t)T + 16u * kg) * kDropC1);
+              uint32_t pv;
+              asm volatile("v_add_u32 %0, %1, %2" : "=v"(pv) : "s"(off), "v"(pre_t));
+              drop_keep_masks(tk2, drop_fin(pv, seed_kx(seed)), km[0], km[1]);
+#else
               uint32_t pv = pre_t;
               asm volatile("" : "+v"(pv));  // hashed here, not hoisted ahead of the tile (its masks would not fit)
               drop_keep_masks(tk2, drop_fin(pv + ((uint32_t)r * (uint32_t)T + 16u * kg) * kDropC1, seed_kx(seed)),
                               km[0], km[1]);
+#endif
             }
 #pragma unroll
             for (int fl = 0; fl < 2; ++fl) {
