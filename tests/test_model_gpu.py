@@ -415,6 +415,40 @@ def test_b64_step_equals_the_mean_of_b4_chunks():
         assert e < 1e-3, (n, e)
 
 
+def test_grouped_weight_gradients_match_the_four_launches():
+    """Round 6: the engine forms a GPT2Block's weight gradients with two grouped launches (fc2 + fc1 after the fc1 dgrad,
+    proj + qkv after the qkv dgrad, gpt2mi_gemm_wgrad_grouped at the pairs' common split count) instead of four
+    gpt2mi_gemm_wgrad launches at their own split counts. On one model and batch (124M widths, 2 layers, B = 8,
+    T = 1024, bf16 autocast): the same loss, the gradients no weight-gradient GEMM forms equal up to the order of their fp32
+    atomics, and the block weight gradients equal to the fp32 rounding of their split-K sums (the pairs sum 7 slabs where
+    qkv / proj summed 9 / 28)."""
+    from gpt_2_distributed_amd.model import GPT2, GPT2Config
+    m = GPT2(GPT2Config(n_layer=2, resid_pdrop=0.0, attn_pdrop=0.0)).to(dev)
+    eng = m.engine()
+    g = torch.Generator().manual_seed(66)
+    t = torch.randint(0, 50257, (8, 1025), generator=g).to(dev)
+    x, y = t[:, :-1].contiguous(), t[:, 1:].contiguous()
+    grads, losses = [], []
+    for grouped in (True, False):
+        eng.GROUP_WGRADS = grouped
+        m.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            _, loss = m(x, labels=y)
+        loss.backward()
+        grads.append(eng.grad.clone())
+        losses.append(loss.item())
+    del eng.GROUP_WGRADS  # back to the class default
+    assert losses[0] == losses[1]
+    wgt = {f"transformer.h.{l}.{n}" for l in range(2)
+           for n in ("attn.qkv.weight", "attn.proj.weight", "mlp.fc1.weight", "mlp.fc2.weight")}
+    for n, sl in m.layout.slots.items():
+        a = grads[0][sl.offset:sl.offset + sl.numel]
+        b = grads[1][sl.offset:sl.offset + sl.numel]
+        # (the others differ at most by the order of the fp32 atomics of the LayerNorm / bias / embedding backwards)
+        e = float((a - b).double().norm() / (b.double().norm() + 1e-30))
+        assert e < (1e-5 if n in wgt else 1e-6), (n, e)
+
+
 def test_lazy_zero_grad_matches_memset():
     """zero_grad(set_to_none=True) before a whole-model backward zeroes only the accumulated slots; the weight-
     gradient GEMMs write theirs. Against a backward into a memset arena: block weight slots bitwise equal (0 + s =
