@@ -113,7 +113,7 @@ int gpt2mi_gemm_wgrad_kt(int M, int N, int K, const uint16_t* A, int lda, const 
                          size_t workspace_floats, int splits, int sched, void* stream);
 
 /* Grouped weight gradients (v13; train_gpt2_distributed.py:412, the autograd wgrads of a GPT2Block's four nn.Linear,
- * model.py:131,135,172,175): for g < count (<= 4), C[g][M[g]][N[g]] (+)= alpha*(alpha_dev?) * A[g]^T B[g] over the same
+ * model.py:95,96,174,177): for g < count (<= 4), C[g][M[g]][N[g]] (+)= alpha*(alpha_dev?) * A[g]^T B[g] over the same
  * K tokens, as ONE split-K launch and ONE reduction launch. Host arrays of count entries; every M[g], N[g] a multiple of
  * 256, K of 128, ldc == N[g]; workspace >= splits * sum(M[g]*N[g]) floats. Each C[g] gets the bits gpt2mi_gemm_wgrad
  * gives it with the same `splits` and fp32 slabs. sched: GPT2MI_SCHED_AUTO or the CU-sharing flags (no BF16_SLABS). */
