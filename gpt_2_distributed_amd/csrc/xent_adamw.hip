@@ -121,6 +121,10 @@ __global__ __launch_bounds__(256) void xent_fwd_kernel(const TL* __restrict__ lo
 // 100 KB row that no longer sits in L2 when its second pass starts: 3 passes of HBM traffic).
 // 60 VGPRs (the row packed, see fence()) = two blocks per CU, so one row's load phase overlaps another's
 // store phase (2611 -> 2494 us at cfg 2's head; at 90 VGPRs a CU held one row at a time).
+#ifndef XENT_EXP_ONCE
+#define XENT_EXP_ONCE 0  // A/B builds: 1 = one exp per logit (the row replaced by its bf16 exp(v - max))
+#endif
+GPT2MI_PRODUCT_KNOB(XENT_EXP_ONCE, 0);
 template <int NCH>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8)))
 void xent_row_kernel(const bf16* __restrict__ logits, int ld, const int64_t* __restrict__ labels,
@@ -130,6 +134,7 @@ void xent_row_kernel(const bf16* __restrict__ logits, int ld, const int64_t* __r
   const bf16* lp = logits + (size_t)row * ld;
   __shared__ float red[16];
   __shared__ float s_bcast;
+  [[maybe_unused]] __shared__ float s_inv_sum;
   bf16x8 raw[NCH];  // the row, packed (4 VGPRs per chunk of 8)
 #pragma unroll
   for (int i = 0; i < NCH; ++i) {
@@ -169,10 +174,23 @@ void xent_row_kernel(const bf16* __restrict__ logits, int ld, const int64_t* __r
   __syncthreads();
   const float mx = s_bcast;
   float sum = 0.f;
+#if XENT_EXP_ONCE
+  // (A/B timing build) the row's exp(v - max) replaces it in the packed registers (bf16): dlogits is then one multiply
+  // by 1/sum per element instead of a second exp (one more bf16 rounding than the product kernel's)
+#pragma unroll
+  for (int i = 0; i < NCH; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float e = __expf(val(i, j) - mx);
+      sum += e;
+      raw[i][j] = f2bf(e);
+    }
+#else
 #pragma unroll
   for (int i = 0; i < NCH; ++i)
 #pragma unroll
     for (int j = 0; j < 8; ++j) sum += __expf(val(i, j) - mx);  // exp(-inf) = 0 for the padding
+#endif
   fence();
   sum = wave_sum(sum);
   __syncthreads();  // s_bcast consumed
@@ -183,6 +201,9 @@ void xent_row_kernel(const bf16* __restrict__ logits, int ld, const int64_t* __r
     for (int k = 0; k < 16; ++k) t += red[k];
     const float lse = mx + __logf(t);
     s_bcast = lse;
+#if XENT_EXP_ONCE
+    s_inv_sum = 1.f / t;
+#endif
     lse_out[row] = lse;
     const int64_t y = labels[row];
     loss_rows[row] = (y == ignore_index) ? 0.f : (y < 0 || y >= V) ? __builtin_nanf("") : lse - bf2f(lp[y]);
@@ -192,6 +213,7 @@ void xent_row_kernel(const bf16* __restrict__ logits, int ld, const int64_t* __r
   const int64_t y = labels[row];
   const bool ign = (y == ignore_index);
   const float lse = (!ign && (y < 0 || y >= V)) ? __builtin_nanf("") : s_bcast;  // bad label: NaN row
+  [[maybe_unused]] const float s_inv = (!ign && (y < 0 || y >= V)) ? __builtin_nanf("") : s_inv_sum;
   bf16* dp = dlogits + (size_t)row * ldd;
 #pragma unroll
   for (int i = 0; i < NCH; ++i) {
@@ -199,7 +221,11 @@ void xent_row_kernel(const bf16* __restrict__ logits, int ld, const int64_t* __r
     if (c >= ldd) continue;
     bf16x8 o;
 #pragma unroll
+#if XENT_EXP_ONCE
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(ign ? 0.f : val(i, j) * s_inv);
+#else
     for (int j = 0; j < 8; ++j) o[j] = f2bf(ign ? 0.f : __expf(val(i, j) - lse));
+#endif
     if (!ign && (uint32_t)(y - c) < 8u) o[y - c] = f2bf(bf2f(o[y - c]) - 1.f);
     *reinterpret_cast<bf16x8*>(dp + c) = o;
   }
