@@ -1,4 +1,4 @@
-"""Multi-process data-parallel logic on CPU with gloo (world sizes 2 and 3): the bucketed SUM
+"""Multi-process data-parallel logic on CPU with gloo (world sizes 2, 3 and the 8 of the BASELINE node): the bucketed SUM
 all-reduce over a flat arena (DDP path), the FSDP shard plan (any world size) and its bf16/fp32
 reduce-scatter / all-gather round trip. Gradients reach the collectives pre-divided by world (the
 engine's GradHooks.begin_backward), so a SUM is the average on every backend; the identity the DDP
@@ -89,8 +89,9 @@ def test_bucketed_allreduce_deferred_last_bucket_gloo():
         assert (lo, hi) == (0, 1000)  # the embeddings' range (first in the arena, final last)
 
 
-def test_bucketed_allreduce_gloo():
-    out = _spawn(_bucketed)
+@pytest.mark.parametrize("world", [2, 8])  # 8: the rank count of the BASELINE node, rehearsed on CPU
+def test_bucketed_allreduce_gloo(world):
+    out = _spawn(_bucketed, world)
     for r, v in out.items():
         assert isinstance(v, tuple), v
         ok, n_launched, was_reset = v
@@ -196,7 +197,7 @@ def _shard_math(rank, world):
     return ok
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_reduce_scatter_all_gather_gloo(world):
     out = _spawn(_shard_math, world)
     assert all(v is True for v in out.values()), out
