@@ -224,7 +224,7 @@ def test_resharded_inner_parameters_expose_no_gradient(results):
 
 
 WIDE = {name: json.load(open(os.path.join(GOLDEN, name)))
-        for name in ("cfg5_golden.json", "cfg4_golden.json", "ddp124_golden.json")}
+        for name in ("cfg5_golden.json", "cfg4_golden.json", "ddp124_golden.json", "ddp_golden.json")}
 WIDE_RUNS = {  # (golden file, ranks, backend, variants, extra env)
     "cfg5_gloo2": ("cfg5_golden.json", 2, "gloo", ["fsdp/fused/fp32", "fsdp/fused/bf16", "fsdp/torch/fp32",
                                                     "fsdp/reshard/fp32", "fsdp/reshard/bf16"], {}),
@@ -238,21 +238,42 @@ WIDE_RUNS = {  # (golden file, ranks, backend, variants, extra env)
                                                         "ddp/torch/fp32"], {"BUCKET_MB": "25"}),
     "ddp124_rccl1": ("ddp124_golden.json", 1, "nccl", ["ddp/fused/bf16", "ddp/overlap/bf16"], {"BUCKET_MB": "25"}),
 }
+# four ranks sharing the GPU (round 6): the collectives' rank count beyond two, on the real engine — DDP at the 124M
+# widths with torch's 25 MiB buckets, and the small golden through DDP and FSDP resident / FULL_SHARD
+FOUR_RUNS = {
+    "ddp124_gloo4": ("ddp124_golden.json", 4, "gloo", ["ddp/fused/bf16", "ddp/overlap/bf16", "ddp/fused/fp32"],
+                     {"BUCKET_MB": "25"}),
+    "small_gloo4": ("ddp_golden.json", 4, "gloo", ["ddp/fused/fp32", "fsdp/fused/fp32", "fsdp/overlap/bf16",
+                                                    "fsdp/reshard/fp32", "fsdp/reshard/bf16"], {}),
+}
+
+
+def _launch_runs(tmp_path_factory, runs, port0):
+    out = {}
+    for i, (run, (gold, nproc, backend, variants, extra)) in enumerate(runs.items()):
+        env = dict(GPT2MI_DIST_BACKEND=backend, **extra)
+        if nproc > 1:
+            env["GPT2MI_SINGLE_DEVICE"] = "1"
+        else:
+            env["GPT2MI_FORCE_COLLECTIVES"] = "1"
+        out[run] = _launch(tmp_path_factory.mktemp(run), nproc, variants, port0 + i, golden=gold, **env)
+        # progress past pytest's capture: a long fixture otherwise prints nothing until its first test reports
+        print(f"[test_ddp_gpu] {run}: {len(variants)} variants done", file=sys.__stderr__, flush=True)
+    return out
 
 
 @pytest.fixture(scope="module")
 def wide_results(tmp_path_factory):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    out = {}
-    for i, (run, (gold, nproc, backend, variants, extra)) in enumerate(WIDE_RUNS.items()):
-        env = dict(GPT2MI_DIST_BACKEND=backend, **extra)
-        if nproc > 1:
-            env["GPT2MI_SINGLE_DEVICE"] = "1"
-        else:
-            env["GPT2MI_FORCE_COLLECTIVES"] = "1"
-        out[run] = _launch(tmp_path_factory.mktemp(run), nproc, variants, 29560 + i, golden=gold, **env)
-    return out
+    return _launch_runs(tmp_path_factory, WIDE_RUNS, 29560)
+
+
+@pytest.fixture(scope="module")
+def four_results(tmp_path_factory):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return _launch_runs(tmp_path_factory, FOUR_RUNS, 29580)
 
 
 @pytest.mark.parametrize("run,variant", [(r, v) for r, spec in WIDE_RUNS.items() for v in spec[3]])
@@ -262,6 +283,15 @@ def test_production_width_vs_reference(wide_results, run, variant):
     grad norm and final parameters, fp32 within 1e-4 and bf16 autocast within 2e-2."""
     gold, nproc = WIDE_RUNS[run][0], WIDE_RUNS[run][1]
     _check_vs_golden(wide_results[run][variant], variant, GOLD=WIDE[gold], world=nproc)
+
+
+@pytest.mark.parametrize("run,variant", [(r, v) for r, spec in FOUR_RUNS.items() for v in spec[3]])
+def test_four_ranks_vs_reference(four_results, run, variant):
+    """Four ranks on gloo sharing the GPU, against the reference on the concatenated batch (the goldens' rows split
+    four ways): DDP at 124M widths with 25 MiB buckets, and DDP / FSDP resident / FSDP FULL_SHARD on the small
+    golden — the shard plan, gathers, reduce-scatters and staging rings at a rank count beyond two."""
+    gold, nproc = FOUR_RUNS[run][0], FOUR_RUNS[run][1]
+    _check_vs_golden(four_results[run][variant], variant, GOLD=WIDE[gold], world=nproc)
 
 
 @pytest.mark.parametrize("parallel", ["ddp", "fsdp"])
