@@ -27,6 +27,8 @@ Outputs (all small data files, no reference source):
   cfg4_golden.json  the same identity at BASELINE cfg 4's widths (GPT-2 350M: C=1024, H=16, V=50257, T=1024) on 2
                     layers, 2 ranks x B=1, grad_accum=2, 3 steps, lr 1e-3, Zipf tokens stored in the file: the FSDP
                     (FULL_SHARD) test of the 350M configuration (train_gpt2_distributed.py:146-161).
+  ddp8_golden.json  ddp_golden.json's configuration over 8 rows per micro-batch (8 ranks x B=1; round 6): the
+                    eight-rank test on gloo ranks sharing one GPU.
 """
 from __future__ import annotations
 
@@ -133,7 +135,7 @@ def tiny_accum(steps=6, grad_accum=4):
 DDPCFG = dict(n_layer=2, n_head=4, n_embd=256, vocab_size=509, n_positions=64, resid_pdrop=0.0, attn_pdrop=0.0)
 
 
-def ddp_golden(steps=3, grad_accum=2, world=2, per_rank=2):
+def ddp_golden(steps=3, grad_accum=2, world=2, per_rank=2, name="ddp_golden.json"):
     """Single-process reference on the concatenated batch: rank r's micro-batch a of step s is
     toks[s, a, r*per_rank:(r+1)*per_rank] (torch.Generator().manual_seed(5), the tests' generator)."""
     cfg = ref_model.GPT2Config(**DDPCFG)
@@ -143,13 +145,19 @@ def ddp_golden(steps=3, grad_accum=2, world=2, per_rank=2):
                for s in range(steps) for a in range(grad_accum)]
     ms = []
     losses, norms = _ref_traj(cfg, batches, steps, grad_accum=grad_accum, lr=1e-3, model_out=ms)
-    with open(os.path.join(HERE, "ddp_golden.json"), "w") as f:
+    with open(os.path.join(HERE, name), "w") as f:
         json.dump({"config": DDPCFG, "world": world, "per_rank": per_rank, "grad_accum": grad_accum,
                    "steps": steps, "lr": 1e-3,
                    "data": "torch.randint(0,509,(steps,grad_accum,world*per_rank,65), Generator seed 5); rank r "
                            "takes rows r*per_rank..", "losses": losses, "grad_norms": norms,
                    "params": _param_checks(ms[0])}, f, indent=0)
-    print("ddp golden", losses, norms)
+    print(name, losses, norms)
+
+
+def ddp8_golden():
+    """The DDP golden over 8 rows of each micro-batch (round 6): eight ranks of one row each, the rank count of the
+    BASELINE node, rehearsed on gloo ranks sharing one GPU (tests/test_ddp_gpu.py EIGHT_RUNS)."""
+    ddp_golden(world=8, per_rank=1, name="ddp8_golden.json")
 
 
 def _wide_golden(name, cfg_kw, seq_len, steps, grad_accum, world, per_rank, lr, seed):
@@ -269,7 +277,7 @@ if __name__ == "__main__":
     a = ap.parse_args()
     jobs = {"tiny": tiny_fwd_bwd, "tinytraj": tiny_traj, "init": init_124m, "loader": loader_grid,
             "traj": traj_124m, "accum": tiny_accum, "ddp": ddp_golden, "cfg5": cfg5_golden,
-            "ddp124": ddp124_golden, "cfg4": cfg4_golden}
+            "ddp124": ddp124_golden, "cfg4": cfg4_golden, "ddp8": ddp8_golden}
     for k, fn in jobs.items():
         if a.only and k not in a.only.split(","):
             continue

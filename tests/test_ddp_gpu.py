@@ -224,7 +224,8 @@ def test_resharded_inner_parameters_expose_no_gradient(results):
 
 
 WIDE = {name: json.load(open(os.path.join(GOLDEN, name)))
-        for name in ("cfg5_golden.json", "cfg4_golden.json", "ddp124_golden.json", "ddp_golden.json")}
+        for name in ("cfg5_golden.json", "cfg4_golden.json", "ddp124_golden.json", "ddp_golden.json",
+                     "ddp8_golden.json")}
 WIDE_RUNS = {  # (golden file, ranks, backend, variants, extra env)
     "cfg5_gloo2": ("cfg5_golden.json", 2, "gloo", ["fsdp/fused/fp32", "fsdp/fused/bf16", "fsdp/torch/fp32",
                                                     "fsdp/reshard/fp32", "fsdp/reshard/bf16"], {}),
@@ -245,6 +246,9 @@ FOUR_RUNS = {
                      {"BUCKET_MB": "25"}),
     "small_gloo4": ("ddp_golden.json", 4, "gloo", ["ddp/fused/fp32", "fsdp/fused/fp32", "fsdp/overlap/bf16",
                                                     "fsdp/reshard/fp32", "fsdp/reshard/bf16"], {}),
+    # eight ranks, the rank count of the BASELINE node, one row each (ddp8_golden.json: the reference on the 8 rows)
+    "small_gloo8": ("ddp8_golden.json", 8, "gloo", ["ddp/fused/fp32", "ddp/overlap/bf16", "fsdp/fused/fp32",
+                                                     "fsdp/reshard/bf16"], {}),
 }
 
 
@@ -287,9 +291,9 @@ def test_production_width_vs_reference(wide_results, run, variant):
 
 @pytest.mark.parametrize("run,variant", [(r, v) for r, spec in FOUR_RUNS.items() for v in spec[3]])
 def test_four_ranks_vs_reference(four_results, run, variant):
-    """Four ranks on gloo sharing the GPU, against the reference on the concatenated batch (the goldens' rows split
-    four ways): DDP at 124M widths with 25 MiB buckets, and DDP / FSDP resident / FSDP FULL_SHARD on the small
-    golden — the shard plan, gathers, reduce-scatters and staging rings at a rank count beyond two."""
+    """Four and eight ranks on gloo sharing the GPU, against the reference on the concatenated batch (the goldens' rows
+    split four / eight ways): DDP at 124M widths with 25 MiB buckets, and DDP / FSDP resident / FSDP FULL_SHARD on the
+    small goldens — the shard plan, gathers, reduce-scatters and staging rings at rank counts beyond two."""
     gold, nproc = FOUR_RUNS[run][0], FOUR_RUNS[run][1]
     _check_vs_golden(four_results[run][variant], variant, GOLD=WIDE[gold], world=nproc)
 

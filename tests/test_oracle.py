@@ -222,10 +222,11 @@ def test_grad_accumulation_matches_reference():
     _check_params(params, ref["params"], 1e-4)
 
 
-def test_ddp_golden_is_the_concatenated_batch_run():
-    """tests/golden/ddp_golden.json (the reference on the 2-rank concatenated batch) is what the oracle
-    computes from the same per-rank micro-batches, concatenated in rank order."""
-    ref = json.load(open(os.path.join(GOLDEN, "ddp_golden.json")))
+@pytest.mark.parametrize("name", ["ddp_golden.json", "ddp8_golden.json"])
+def test_ddp_golden_is_the_concatenated_batch_run(name):
+    """tests/golden/ddp_golden.json / ddp8_golden.json (the reference on the 2-rank / 8-rank concatenated batch) is what
+    the oracle computes from the same per-rank micro-batches, concatenated in rank order."""
+    ref = json.load(open(os.path.join(GOLDEN, name)))
     cfg = model_ref.Cfg(**ref["config"])
     S, GA, W, P = ref["steps"], ref["grad_accum"], ref["world"], ref["per_rank"]
     toks = torch.randint(0, 509, (S, GA, W * P, 65), generator=torch.Generator().manual_seed(5))
