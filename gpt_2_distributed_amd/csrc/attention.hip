@@ -49,6 +49,7 @@ GPT2MI_PRODUCT_KNOB(ATTN_DKDV_PIPE, 0);
 #ifndef ATTN_HASH_ANCHOR
 #define ATTN_HASH_ANCHOR 0  // dK/dV dropout hash: 1 = the opaque anchor on the counter sum (no v_mov per hash; A/B)
 #endif
+GPT2MI_PRODUCT_KNOB(ATTN_HASH_ANCHOR, 0);
 constexpr int kThreads = 256;
 constexpr float kLog2e = 1.4426950408889634f;
 
