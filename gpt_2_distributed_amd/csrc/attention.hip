@@ -50,6 +50,16 @@ GPT2MI_PRODUCT_KNOB(ATTN_DKDV_PIPE, 0);
 #define ATTN_HASH_ANCHOR 0  // dK/dV dropout hash: 1 = the opaque anchor on the counter sum (no v_mov per hash; A/B)
 #endif
 GPT2MI_PRODUCT_KNOB(ATTN_HASH_ANCHOR, 0);
+#ifndef ATTN_DQ_SGB
+#define ATTN_DQ_SGB 0  // dQ tile: 1 = sched_group_barrier interleave of each half's MFMAs with the other half's VALU (A/B)
+#endif
+#ifndef ATTN_DQ_FA
+#define ATTN_DQ_FA 6  // ATTN_DQ_SGB: VALU instructions after each S / dP MFMA of the second half
+#endif
+#ifndef ATTN_DQ_FB
+#define ATTN_DQ_FB 12  // ATTN_DQ_SGB: VALU instructions after each dQ MFMA of the first half
+#endif
+GPT2MI_PRODUCT_KNOB(ATTN_DQ_SGB, 0);
 constexpr int kThreads = 256;
 constexpr float kLog2e = 1.4426950408889634f;
 
@@ -521,12 +531,36 @@ __global__ __launch_bounds__(kThreads, 3) void attn_bwd_dq_kernel(const bf16* __
         f32x4 sa[2][2], dpa[2][2], sb[2][2], dpb[2][2];
         bf16x8 pa[2], pb[2];
         sdp(0, sa, dpa);
+#if ATTN_DQ_SGB
+        // A/B: the second half's S / dP MFMAs placed one by one among the first half's dS chain, then the first half's
+        // dQ MFMAs among the second half's chain (fragment reads first in each region)
+        __builtin_amdgcn_sched_barrier(0);
+        elem(diag_c, 0, sa, dpa, pa);
+        sdp(1, sb, dpb);
+        __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, ATTN_DQ_FA, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        dqm(0, pa);
+        elem(diag_c, 1, sb, dpb, pb);
+        __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, ATTN_DQ_FB, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#else
         elem(diag_c, 0, sa, dpa, pa);
         sdp(1, sb, dpb);
         __builtin_amdgcn_sched_barrier(0);
         dqm(0, pa);
         elem(diag_c, 1, sb, dpb, pb);
         __builtin_amdgcn_sched_barrier(0);
+#endif
         dqm(1, pb);
       };
       if (diag) tile(std::true_type{});
